@@ -1,0 +1,129 @@
+"""ctypes front-end of the C oracle (tdec_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- the parity checker and the "port" CPU baseline.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle_tdec.so")
+_lib = None
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        L.orc_trellis.argtypes = [_i32p, _i32p]
+        L.orc_interleaver.argtypes = [C.c_int, _i32p, _i32p, _i32p]
+        L.orc_siso.argtypes = [C.c_int, _f32p, _f32p, _f32p, _f32p, _f64p, _f64p, _i32p,
+                               C.c_double, C.c_int, _f64p, _f64p]
+        L.orc_decode.argtypes = [C.c_int, C.c_int, _u8p, C.c_int, C.c_int, _i32p, _i32p, _i32p,
+                                 _f32p, C.c_long, _i32p, C.c_void_p]
+        L.orc_decode.restype = C.c_int
+        L.orc_decode_batch.argtypes = [C.c_int, C.c_int, C.c_int, _u8p, C.c_int, C.c_int, _i32p, _i32p,
+                                       _i32p, _f32p, C.c_long, C.c_long, _i32p, C.c_void_p, C.c_int]
+        L.orc_decode_batch.restype = C.c_int
+        L.orc_encode.argtypes = [C.c_int, C.c_int, _u8p, _i32p, _i32p, _i32p, _i32p, _i32p]
+        L.orc_encode.restype = C.c_long
+        L.orc_demap_c64.argtypes = [_f32p, C.c_long, _f32p, C.c_int, C.c_int, C.c_double, C.c_int, _f64p]
+        L.orc_demap_c128.argtypes = [_f64p, C.c_long, _f64p, C.c_int, C.c_int, C.c_double, _f64p]
+        _lib = L
+    return _lib
+
+
+def trellis():
+    t = np.zeros((5, 16, 4), np.int32)
+    G = np.zeros((4, 4), np.int32)
+    lib().orc_trellis(t, G)
+    return t, G
+
+
+def interleaver(n, params):
+    perm = np.zeros(n, np.int32)
+    inv = np.zeros(n, np.int32)
+    lib().orc_interleaver(n, np.asarray(params, np.int32), perm, inv)
+    return perm, inv
+
+
+def siso(LcA, LcB, LcW, LcY, LaA, LaB, tables, sf, algo=0):
+    n = len(LcA)
+    c = lambda x, dt: np.ascontiguousarray(x, dt)
+    LeA = np.zeros(n)
+    LeB = np.zeros(n)
+    lib().orc_siso(n, c(LcA, np.float32), c(LcB, np.float32), c(LcW, np.float32), c(LcY, np.float32),
+                   c(LaA, np.float64), c(LaB, np.float64), c(tables, np.int32), float(sf), algo, LeA, LeB)
+    return LeA, LeB
+
+
+def decode(llr, n, period, punct, iterations, perm, inv, tables, algo=0, want_lfinal=False):
+    llr = np.ascontiguousarray(llr, np.float32)
+    bits = np.zeros(2 * n, np.int32)
+    lf = np.zeros(2 * n) if want_lfinal else None
+    rc = lib().orc_decode(n, period, np.ascontiguousarray(punct, np.uint8), iterations, algo,
+                          np.ascontiguousarray(perm, np.int32), np.ascontiguousarray(inv, np.int32),
+                          np.ascontiguousarray(tables, np.int32), llr, llr.size, bits,
+                          lf.ctypes.data if lf is not None else None)
+    if rc:
+        raise IndexError("llr too short") if rc == -1 else ValueError(f"oracle error {rc}")
+    return (bits, lf) if want_lfinal else bits
+
+
+def decode_batch(llr, n, period, punct, iterations, perm, inv, tables, algo=0, nthreads=0,
+                 want_lfinal=False):
+    llr = np.ascontiguousarray(llr, np.float32)
+    B = llr.shape[0]
+    bits = np.zeros((B, 2 * n), np.int32)
+    lf = np.zeros((B, 2 * n)) if want_lfinal else None
+    rc = lib().orc_decode_batch(B, n, period, np.ascontiguousarray(punct, np.uint8), iterations, algo,
+                                np.ascontiguousarray(perm, np.int32), np.ascontiguousarray(inv, np.int32),
+                                np.ascontiguousarray(tables, np.int32), llr, llr.shape[1], llr.shape[1],
+                                bits, lf.ctypes.data if lf is not None else None, nthreads)
+    if rc:
+        raise ValueError(f"oracle error {rc}")
+    return (bits, lf) if want_lfinal else bits
+
+
+def encode(bits, n, period, punct, perm, tables, G):
+    bits = np.ascontiguousarray(bits, np.int32)
+    out = np.zeros(6 * n + 8, np.int32)
+    m = lib().orc_encode(n, period, np.ascontiguousarray(punct, np.uint8), np.ascontiguousarray(perm, np.int32),
+                         np.ascontiguousarray(tables, np.int32), np.ascontiguousarray(G, np.int32), bits, out)
+    return out[:m].copy()
+
+
+def demap(syms, constellation, bps, noise_var, div_f32=False):
+    """compute_llr semantics; the arithmetic dtype is numpy's promotion of
+    (symbols, constellation).  div_f32: noise_var was a Python float and the
+    arithmetic is complex64 (NEP 50 keeps min_d0 - min_d1 in float32)."""
+    syms = np.asarray(syms)
+    constellation = np.asarray(constellation)
+    M = len(constellation)
+    out = np.zeros(len(syms) * bps)
+    if syms.dtype == np.complex128 or constellation.dtype == np.complex128:
+        s = np.ascontiguousarray(syms.astype(np.complex128).view(np.float64))
+        cons = np.ascontiguousarray(constellation.astype(np.complex128).view(np.float64))
+        lib().orc_demap_c128(s, len(syms), cons, M, bps, float(noise_var), out)
+        return out
+    s = np.ascontiguousarray(syms.astype(np.complex64).view(np.float32))
+    cons = np.ascontiguousarray(constellation.astype(np.complex64).view(np.float32))
+    lib().orc_demap_c64(s, len(syms), cons, M, bps, float(noise_var), int(div_f32), out)
+    return out

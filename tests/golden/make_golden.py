@@ -1,0 +1,297 @@
+#!/usr/bin/env python3
+"""Generate the committed golden vectors for the turbo-decode hot path.
+
+TEST INFRASTRUCTURE ONLY.  This script runs in the survey/build container,
+where the read-only reference checkout lives at /root/reference.  It imports
+the reference's ``dvb_rcs2_turbo`` module unmodified, with a no-op ``numba``
+stand-in (``njit`` = identity) so the numba kernels run as plain
+CPython + numpy.  SURVEY.md §8(c) records that this shim is bit-identical to
+the author's cached numba machine code for ``bcjr_max_log_map``.
+
+The reference never travels to the GPU box: only the ``*.npz`` files written
+here (inputs and expected outputs, no code) do.
+
+Which inverse interleaver a vector used is recorded per file
+(``inv_perm`` key), because ``np.argsort(perm)`` of the reference
+(dvb_rcs2_turbo.py:325) breaks ties differently per numpy SIMD path
+(SURVEY.md fact 4).  ``inv_stable`` = ``np.argsort(perm, kind='stable')`` is the
+build's canonical pin; ``inv_default`` is what this container's numpy
+(2.2.6, AVX-512) returns for the reference's unstable argsort.
+
+Usage:  python tests/golden/make_golden.py   (takes a few minutes)
+"""
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+N_ALL = [48, 64, 212, 220, 424, 752, 848]
+
+
+def _import_reference():
+    shim = tempfile.mkdtemp(prefix="numba_shim_")
+    os.makedirs(os.path.join(shim, "numba"))
+    with open(os.path.join(shim, "numba", "__init__.py"), "w") as f:
+        f.write(
+            "def njit(*a, **k):\n"
+            "    if len(a) == 1 and callable(a[0]) and not k:\n"
+            "        return a[0]\n"
+            "    return lambda f: f\n"
+            "int32 = float32 = float64 = int64 = None\n"
+        )
+    sys.path[:0] = [shim, REF]
+    sys.dont_write_bytecode = True
+    import dvb_rcs2_turbo as T  # noqa: E402
+    return T
+
+
+def make_codec(T, n, rate, iterations=8):
+    """Construct without the (slow, pure-Python) JIT warm-up decode."""
+    orig = T.DVBRCS2_Turbo.decode
+    T.DVBRCS2_Turbo.decode = lambda self, llr: None
+    try:
+        c = T.DVBRCS2_Turbo(n, rate, iterations)
+    finally:
+        T.DVBRCS2_Turbo.decode = orig
+    return c
+
+
+def gen_tables(T):
+    c = make_codec(T, 48, "1/3")
+    out = dict(
+        next_state=c.next_state, out_W=c.out_W, out_Y=c.out_Y,
+        prev_state=c.prev_state, prev_input=c.prev_input, G=c.G_matrix,
+        N_all=np.array(N_ALL, np.int32),
+        interleaver_params=np.array([T.INTERLEAVER_PARAMS[n] for n in N_ALL], np.int32),
+    )
+    for n in N_ALL:
+        cc = make_codec(T, n, "1/3")
+        out[f"perm_{n}"] = cc.perm
+        out[f"inv_default_{n}"] = cc.inv_perm
+        out[f"inv_stable_{n}"] = np.argsort(cc.perm, kind="stable").astype(np.int32)
+        for rate in ("1/3", "1/2", "2/3", "3/4"):
+            out[f"n_coded_{n}_{rate.replace('/', '_')}"] = np.int64(make_codec(T, n, rate).n_coded)
+    # G^N and the circular-state solution for every Z_N (encoder, :404-429)
+    for n in N_ALL:
+        gp = T.mat_pow_gf2(c.G_matrix, n)
+        out[f"gpow_{n}"] = gp
+        out[f"circ_{n}"] = np.array([T.solve_circular_state_gf2(gp, z) for z in range(16)], np.int32)
+    np.savez_compressed(os.path.join(OUT, "tables.npz"), **out)
+
+
+def gen_encode(T):
+    rng = np.random.default_rng(20251226)
+    out = {}
+    for n, rates in ((48, ("1/3", "1/2", "2/3", "3/4")), (212, ("1/3", "1/2")), (752, ("1/3", "1/2"))):
+        for rate in rates:
+            c = make_codec(T, n, rate)
+            bits = rng.integers(0, 2, (6, c.k_info)).astype(np.int32)
+            coded = np.stack([c.encode(b) for b in bits])
+            key = f"{n}_{rate.replace('/', '_')}"
+            out[f"bits_{key}"] = bits
+            out[f"coded_{key}"] = coded
+    np.savez_compressed(os.path.join(OUT, "encode.npz"), **out)
+
+
+def gen_siso(T):
+    """Per-SISO known answers: bcjr_max_log_map (dvb_rcs2_turbo.py:116-281)."""
+    rng = np.random.default_rng(7)
+    c = make_codec(T, 48, "1/3")
+    tabs = (c.next_state, c.out_W, c.out_Y, c.prev_state, c.prev_input)
+    out = {}
+    for n, count in ((48, 10), (212, 6), (752, 4)):
+        cases = []
+        for i in range(count):
+            sc = [0.5, 2.0, 8.0, 30.0][i % 4]
+            la_sc = [0.0, 5.0, 20.0, 50.0][(i // 2) % 4]
+            Lc = (rng.standard_normal((4, n)) * sc).astype(np.float32)
+            La = rng.standard_normal((2, n)) * la_sc
+            if i == 1:   # all-zero input: ties everywhere
+                Lc[:] = 0
+                La[:] = 0
+            if i == 2:   # saturating extrinsic (clip at +-300) and big parities
+                Lc *= 200
+                La *= 20
+            sf = 0.7 if i % 3 else 1.0
+            cases.append((Lc, La, sf))
+        LcA = np.stack([x[0][0] for x in cases]); LcB = np.stack([x[0][1] for x in cases])
+        LcW = np.stack([x[0][2] for x in cases]); LcY = np.stack([x[0][3] for x in cases])
+        LaA = np.stack([x[1][0] for x in cases]); LaB = np.stack([x[1][1] for x in cases])
+        sf = np.array([x[2] for x in cases])
+        LeA = np.zeros_like(LaA); LeB = np.zeros_like(LaB)
+        for j in range(count):
+            LeA[j], LeB[j] = T.bcjr_max_log_map(LcA[j], LcB[j], LcW[j], LcY[j], LaA[j], LaB[j],
+                                                 *tabs, n, float(sf[j]))
+        out.update({f"LcA_{n}": LcA, f"LcB_{n}": LcB, f"LcW_{n}": LcW, f"LcY_{n}": LcY,
+                    f"LaA_{n}": LaA, f"LaB_{n}": LaB, f"sf_{n}": sf,
+                    f"LeA_{n}": LeA, f"LeB_{n}": LeB})
+    np.savez_compressed(os.path.join(OUT, "siso.npz"), **out)
+
+
+class _Capture:
+    """Wrap T.bcjr_max_log_map (resolved as a module global at call time by
+    DVBRCS2_Turbo.decode, dvb_rcs2_turbo.py:499/515) to record SISO I/O."""
+
+    def __init__(self, T):
+        self.T = T
+        self.fn = T.bcjr_max_log_map
+        self.calls = []
+
+    def __enter__(self):
+        def wrapped(*a):
+            r = self.fn(*a)
+            self.calls.append((a[0], a[4], a[5], r[0], r[1]))
+            return r
+        self.T.bcjr_max_log_map = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        self.T.bcjr_max_log_map = self.fn
+
+
+def _decode_capture(T, c, llr):
+    with _Capture(T) as cap:
+        bits = c.decode(llr)
+    # Final decision (dvb_rcs2_turbo.py:529-530): Lc + La + Le1, La = Le2[inv_perm]
+    LcA1, _, _, Le1A, Le1B = cap.calls[-2]
+    _, _, _, Le2A, Le2B = cap.calls[-1]
+    LcA = LcA1
+    llr32 = np.array(llr, dtype=np.float32)
+    LcB = np.zeros(c.N, np.float32)
+    # recover Lc_B the same way decode() depunctures it (systematic B is the 2nd value of each couple)
+    idx = 0
+    per = c.punct["period"]
+    for i in range(c.N):
+        p = i % per
+        idx += 1
+        LcB[i] = llr32[idx]; idx += 1
+        idx += c.punct["W1"][p] + c.punct["Y1"][p] + c.punct["W2"][p] + c.punct["Y2"][p]
+    LaA = Le2A[c.inv_perm]; LaB = Le2B[c.inv_perm]
+    LfA = LcA + LaA + Le1A
+    LfB = LcB + LaB + Le1B
+    lfinal = np.zeros(2 * c.N)
+    lfinal[0::2] = LfA; lfinal[1::2] = LfB
+    assert np.array_equal(bits[0::2], (LfA < 0).astype(np.int32))
+    return bits, lfinal
+
+
+def _qpsk_llrs(rng, coded, ebn0_db, rate):
+    """AWGN + QPSK LLRs, decoder sign (LLR>0 => bit 0), SURVEY.md §8(d)."""
+    a = coded[0::2]; b = coded[1::2]
+    sym = ((1 - 2.0 * a) + 1j * (1 - 2.0 * b)) / np.sqrt(2)
+    n0 = 1.0 / (rate * 2 * 10 ** (ebn0_db / 10.0))
+    sig = np.sqrt(n0 / 2)
+    y = sym + sig * (rng.standard_normal(sym.shape) + 1j * rng.standard_normal(sym.shape))
+    llr = np.zeros(coded.shape[0], np.float32)
+    llr[0::2] = 2 * np.sqrt(2) * y.real / n0
+    llr[1::2] = 2 * np.sqrt(2) * y.imag / n0
+    return llr
+
+
+def gen_decode(T):
+    """Full-decode known answers: DVBRCS2_Turbo.decode (dvb_rcs2_turbo.py:464-537)."""
+    rng = np.random.default_rng(99)
+    out = {}
+    plan = [(48, "1/3", 6), (48, "1/2", 4), (48, "2/3", 2), (212, "1/3", 4), (212, "1/2", 3),
+            (752, "1/3", 3), (752, "1/2", 2)]
+    for n, rate, count in plan:
+        Rn = {"1/3": 1 / 3, "1/2": 1 / 2, "2/3": 2 / 3, "3/4": 3 / 4}[rate]
+        for variant in ("stable", "default"):
+            if variant == "default" and rate != "1/3":
+                continue
+            c = make_codec(T, n, rate)
+            if variant == "stable":
+                c.inv_perm = np.argsort(c.perm, kind="stable").astype(np.int32)
+            key = f"{n}_{rate.replace('/', '_')}_{variant}"
+            bits_in, llrs, bits_out, lfin, ebn0 = [], [], [], [], []
+            for i in range(count):
+                info = rng.integers(0, 2, c.k_info).astype(np.int32)
+                coded = c.encode(info)
+                e = [0.0, 2.0, 4.0, 99.0][i % 4]
+                if e == 99.0:
+                    llr = (1 - 2.0 * coded).astype(np.float32) * 20.0
+                else:
+                    llr = _qpsk_llrs(rng, coded, e, Rn)
+                if len(llr) < c.n_coded:  # rate-2/3 quirk: encode() length != n_coded
+                    llr = np.pad(llr, (0, c.n_coded - len(llr)))
+                t = time.time()
+                b, lf = _decode_capture(T, c, llr)
+                print(f"  decode {key} #{i} ebn0={e} errs={int((b != info).sum())} "
+                      f"({time.time() - t:.1f}s)", flush=True)
+                bits_in.append(info); llrs.append(llr); bits_out.append(b); lfin.append(lf); ebn0.append(e)
+            out[f"info_{key}"] = np.stack(bits_in)
+            out[f"llr_{key}"] = np.stack(llrs)
+            out[f"bits_{key}"] = np.stack(bits_out)
+            out[f"lfinal_{key}"] = np.stack(lfin)
+            out[f"ebn0_{key}"] = np.array(ebn0)
+            out[f"inv_{key}"] = c.inv_perm
+    # The survey's behavioural KATs: noise-free +-20 LLRs,
+    # info bits from default_rng(1), container-default inv_perm.
+    for n in (48, 212, 752):
+        c = make_codec(T, n, "1/3")
+        info = np.random.default_rng(1).integers(0, 2, c.k_info)
+        coded = c.encode(info)
+        b = c.decode((1 - 2 * coded) * 20.0)
+        out[f"kat_info_{n}"] = info.astype(np.int32)
+        out[f"kat_bits_{n}"] = b
+        out[f"kat_inv_{n}"] = c.inv_perm
+        print(f"  KAT N={n}: {int((b != info).sum())} errors", flush=True)
+    np.savez_compressed(os.path.join(OUT, "decode.npz"), **out)
+
+
+def gen_demap():
+    """compute_llr (test_sdr_with_coding.py:200-225) and the Gray mappers
+    (:25-100; sdr_modem.py:101-220).  test_sdr_with_coding imports a stale
+    name from dvb_rcs2_turbo, which is stubbed before import."""
+    import types
+    import dvb_rcs2_turbo as T
+    T.DVB_RCS2_TurboCodec = None
+    sys.modules.setdefault("matplotlib", types.ModuleType("matplotlib"))
+    mpl = sys.modules["matplotlib"]
+    if not hasattr(mpl, "pyplot"):
+        mpl.pyplot = types.ModuleType("matplotlib.pyplot")
+        sys.modules["matplotlib.pyplot"] = mpl.pyplot
+    import test_sdr_with_coding as H
+    import sdr_modem as SM
+    rng = np.random.default_rng(5)
+    out = {}
+    for mod in ("BPSK", "QPSK", "8PSK", "16QAM"):
+        bps = H.MODULATIONS[mod]["bps"]
+        order = H.MODULATIONS[mod]["order"]
+        all_bits = np.array([list(map(int, format(i, f"0{bps}b"))) for i in range(order)])
+        const = H.MODULATIONS[mod]["mod"](all_bits.flatten()).reshape(-1)
+        out[f"const_{mod}"] = const
+        nsym = 300
+        tx = const[rng.integers(0, order, nsym)]
+        syms = (tx + 0.3 * (rng.standard_normal(nsym) + 1j * rng.standard_normal(nsym))).astype(np.complex64)
+        syms[:4] = const[:4] if order >= 4 else syms[:4]  # exact constellation hits -> ties / zero distances
+        out[f"syms_{mod}"] = syms
+        out[f"llr_f64nv_{mod}"] = H.compute_llr(syms, mod, np.float64(0.137))   # call-site dtype (:464-471)
+        out[f"llr_f64nvsmall_{mod}"] = H.compute_llr(syms, mod, np.float64(0.001))  # floor at 0.005
+        out[f"llr_pyfloat_{mod}"] = H.compute_llr(syms, mod, 0.02)                # python float: f32 division
+        out[f"llr_c128_{mod}"] = H.compute_llr(syms.astype(np.complex128) * (1 + 1e-9), mod, np.float64(0.2))
+    m = SM.SDRModem.__new__(SM.SDRModem)
+    m._init_gray_tables()
+    for mod, bps in (("8PSK", 3), ("16QAM", 4), ("64QAM", 6), ("256QAM", 8)):
+        all_bits = np.array([list(map(int, format(i, f"0{bps}b"))) for i in range(2 ** bps)])
+        out[f"sdrconst_{mod}"] = m.modulate(all_bits.flatten(), mod).reshape(-1)
+    np.savez_compressed(os.path.join(OUT, "demap.npz"), **out)
+
+
+def main():
+    T = _import_reference()
+    t0 = time.time()
+    gen_tables(T); print("tables", time.time() - t0, flush=True)
+    gen_encode(T); print("encode", time.time() - t0, flush=True)
+    gen_siso(T); print("siso", time.time() - t0, flush=True)
+    gen_demap(); print("demap", time.time() - t0, flush=True)
+    gen_decode(T); print("decode", time.time() - t0, flush=True)
+
+
+if __name__ == "__main__":
+    main()

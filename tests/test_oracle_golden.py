@@ -1,0 +1,112 @@
+"""Pin the C oracle (oracle/tdec_oracle.c) to the reference's own outputs.
+
+The golden vectors were produced by importing the reference module itself
+(tests/golden/make_golden.py).  Equality is IEEE ``==`` (np.array_equal), so
++0 and -0 compare equal; every other bit must match.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from modulations_amd import tables as T
+
+RATES = {"1_3": "1/3", "1_2": "1/2", "2_3": "2/3", "3_4": "3/4"}
+
+
+def test_trellis_tables(G_tables):
+    t, G = O.trellis()
+    for i, k in enumerate(("next_state", "out_W", "out_Y", "prev_state", "prev_input")):
+        assert np.array_equal(t[i], G_tables[k])
+    assert np.array_equal(G, G_tables["G"])
+
+
+@pytest.mark.parametrize("n", [48, 64, 212, 220, 424, 752, 848])
+def test_interleaver(G_tables, n):
+    perm, inv = O.interleaver(n, T.INTERLEAVER_PARAMS[n])
+    assert np.array_equal(perm, G_tables[f"perm_{n}"])
+    assert np.array_equal(inv, G_tables[f"inv_stable_{n}"])
+    # the reference interleaver is not a permutation
+    assert len(np.unique(perm)) < n
+    for rate in RATES:
+        assert T.coded_size(n, T.PUNCTURE_PATTERNS[RATES[rate]]) == int(G_tables[f"n_coded_{n}_{rate}"])
+
+
+@pytest.mark.parametrize("n", [48, 212, 752])
+def test_siso_golden(G_siso, n):
+    t, _ = O.trellis()
+    g = G_siso
+    for j in range(g[f"LcA_{n}"].shape[0]):
+        LeA, LeB = O.siso(g[f"LcA_{n}"][j], g[f"LcB_{n}"][j], g[f"LcW_{n}"][j], g[f"LcY_{n}"][j],
+                          g[f"LaA_{n}"][j], g[f"LaB_{n}"][j], t, g[f"sf_{n}"][j])
+        assert np.array_equal(LeA, g[f"LeA_{n}"][j]), (n, j)
+        assert np.array_equal(LeB, g[f"LeB_{n}"][j]), (n, j)
+
+
+def _decode_cases(G_decode):
+    keys = sorted(k[len("llr_"):] for k in G_decode.files if k.startswith("llr_"))
+    return keys
+
+
+def test_decode_golden(G_decode):
+    t, _ = O.trellis()
+    keys = _decode_cases(G_decode)
+    assert keys
+    for key in keys:
+        n_s, r1, r2, variant = key.split("_")
+        n = int(n_s)
+        punct = T.PUNCTURE_PATTERNS[f"{r1}/{r2}"]
+        pm = T.puncture_matrix(punct)
+        perm = T.interleaver(n)
+        inv = G_decode[f"inv_{key}"]
+        for j, llr in enumerate(G_decode[f"llr_{key}"]):
+            bits, lf = O.decode(llr, n, punct["period"], pm, 8, perm, inv, t, want_lfinal=True)
+            assert np.array_equal(bits, G_decode[f"bits_{key}"][j]), (key, j)
+            assert np.array_equal(lf, G_decode[f"lfinal_{key}"][j]), (key, j)
+
+
+@pytest.mark.parametrize("n,errs", [(48, 21), (212, 83), (752, 355)])
+def test_noise_free_kat(G_decode, n, errs):
+    """SURVEY Appendix C behavioural KAT: the broken interleaver leaves errors."""
+    t, G = O.trellis()
+    punct = T.PUNCTURE_PATTERNS["1/3"]
+    pm = T.puncture_matrix(punct)
+    perm = T.interleaver(n)
+    info = G_decode[f"kat_info_{n}"]
+    coded = O.encode(info, n, 1, pm, perm, t, G)
+    bits = O.decode((1 - 2.0 * coded) * 20.0, n, 1, pm, 8, perm, G_decode[f"kat_inv_{n}"], t)
+    assert np.array_equal(bits, G_decode[f"kat_bits_{n}"])
+    assert int((bits != info).sum()) == errs
+    # a valid permutation decodes the same noise-free word perfectly
+    vp = T.valid_interleaver(n)
+    coded = O.encode(info, n, 1, pm, vp, t, G)
+    bits = O.decode((1 - 2.0 * coded) * 20.0, n, 1, pm, 8, vp, np.argsort(vp).astype(np.int32), t)
+    assert int((bits != info).sum()) == 0
+
+
+def test_encode_golden(G_encode):
+    t, G = O.trellis()
+    for k in G_encode.files:
+        if not k.startswith("bits_"):
+            continue
+        key = k[len("bits_"):]
+        n_s, r1, r2 = key.split("_")
+        n = int(n_s)
+        punct = T.PUNCTURE_PATTERNS[f"{r1}/{r2}"]
+        pm = T.puncture_matrix(punct)
+        for b, c in zip(G_encode[k], G_encode[f"coded_{key}"]):
+            assert np.array_equal(O.encode(b, n, punct["period"], pm, T.interleaver(n), t, G), c), key
+
+
+@pytest.mark.parametrize("mod,bps", [("BPSK", 1), ("QPSK", 2), ("8PSK", 3), ("16QAM", 4)])
+def test_demap_golden(G_demap, mod, bps):
+    g = G_demap
+    cons = g[f"const_{mod}"]
+    syms = g[f"syms_{mod}"]
+    for key, nv in (("f64nv", np.float64(0.137)), ("f64nvsmall", np.float64(0.001)), ("pyfloat", 0.02)):
+        # max(noise_var, 0.005) (:202) returns the Python float 0.005 when it wins, and
+        # numpy >= 2 then keeps float32 for min_d0 - min_d1 divided by it.
+        nv_eff = max(nv, 0.005)
+        div_f32 = (np.float32(1) / nv_eff).dtype == np.float32
+        assert np.array_equal(O.demap(syms, cons, bps, nv_eff, div_f32=div_f32), g[f"llr_{key}_{mod}"]), key
+    s128 = syms.astype(np.complex128) * (1 + 1e-9)
+    assert np.array_equal(O.demap(s128, cons, bps, 0.2), g[f"llr_c128_{mod}"])

@@ -1,0 +1,119 @@
+/*
+ * tdec.h -- C ABI of the MI355X (gfx950) DVB-RCS2 duo-binary turbo decoder.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (poriya219/modulations, dvb_rcs2_turbo.py) has no FFI layer: its boundary is
+ * the Python API of the module.  Each entry point below states which reference
+ * interface it replaces; modulations_amd/dvb_rcs2_turbo.py binds them with
+ * ctypes (INTEGRATION.md shows the binding a maintainer would add to the
+ * reference module itself).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Row-major, batch-major [B][...].
+ *   - Entry points without a _dev suffix take HOST pointers and are
+ *     synchronous.  _dev entry points take DEVICE pointers and a hipStream_t
+ *     (passed as void*), are stream-ordered, never allocate and never
+ *     synchronise once tdec_reserve() has sized the workspace.
+ *   - Return 0 on success, a negative TDEC_E* code otherwise;
+ *     tdec_last_error() (thread-local) says why.  No exception crosses the ABI.
+ *   - A handle is bound to one device.  Calls on different handles may run
+ *     concurrently from different host threads.
+ *   - LLR sign: LLR = log P(0)/P(1) (positive -> bit 0), as the decoder of the
+ *     reference (dvb_rcs2_turbo.py:533-535).
+ */
+#ifndef TDEC_H
+#define TDEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tdec_ctx tdec_t;
+
+enum {
+    TDEC_OK = 0,
+    TDEC_EINVAL = -1,       /* bad argument (bad N, period, tables, null pointer) -> ValueError */
+    TDEC_ESHORT = -2,       /* LLR vector shorter than the de-puncture walk     -> IndexError */
+    TDEC_ENOMEM = -3,       /* device allocation failed                          -> MemoryError */
+    TDEC_EHIP = -4,         /* HIP runtime error                                 -> RuntimeError */
+    TDEC_EUNSUPPORTED = -5, /* trellis tables other than the DVB-RCS2 16-state CRSC */
+    TDEC_EITER = -6,        /* iterations < 1 (the reference raises UnboundLocalError) */
+    TDEC_ECAPACITY = -7     /* _dev call larger than tdec_reserve()                */
+};
+
+enum { TDEC_ALGO_MAXLOG = 0, TDEC_ALGO_LOGMAP = 1 };
+
+/* Codec construction: replaces DVBRCS2_Turbo.__init__ (dvb_rcs2_turbo.py:288-309)
+ * for the decode side.  punct = [4][4] uint8 (rows W1, Y1, W2, Y2; columns the
+ * pattern phase, PUNCTURE_PATTERNS :21-26), period in 1..4.  perm / inv_perm =
+ * int32[n_couples] (the reference's self.perm / self.inv_perm, :311-325).
+ * tables = int32[5][16][4]: next_state, out_W, out_Y, prev_state, prev_input
+ * (:327-396); anything but the DVB-RCS2 trellis returns TDEC_EUNSUPPORTED. */
+int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int iterations, int algo,
+                const int32_t *perm, const int32_t *inv_perm, const int32_t *tables, tdec_t **out);
+void tdec_destroy(tdec_t *h);
+const char *tdec_last_error(void);
+
+/* LLRs one decode reads (the de-puncture walk, :476-487). */
+long tdec_llr_len(const tdec_t *h);
+
+/* One SISO pass over B codewords: replaces bcjr_max_log_map
+ * (dvb_rcs2_turbo.py:116-281; historic name bcjr_decode_circular).
+ * All arrays [B][n_couples], host memory.  Outputs f64 extrinsics. */
+int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
+                    const double *LaA, const double *LaB, double sf, double *LeA, double *LeB);
+
+/* Full turbo decode of B codewords: replaces DVBRCS2_Turbo.decode
+ * (dvb_rcs2_turbo.py:464-537; historic name turbo_decode).  llr rows of
+ * llr_stride floats (>= tdec_llr_len), bits int32[B][2N] (A, B interleaved as
+ * :534-535), lfinal (nullable) f64[B][2N] = Lc + La + Le1 (:529-530). */
+int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32_t *bits, double *lfinal);
+
+/* ---- device-pointer, stream-ordered API (what bench.py and multi-GPU use) ---- */
+
+/* Size the workspace for batches of up to max_batch codewords. */
+int tdec_reserve(tdec_t *h, int max_batch);
+/* Bytes of the de-punctured plane buffer for B codewords.  Layout (opaque to
+ * callers): [ceil(B/64)][2][N][64] float4 -- per 64-codeword tile and trellis
+ * step, {A, B, W1, Y1} and {A[perm], B[perm], W2, Y2}.  tdec_decode_planes_dev
+ * completes the second vector in place (the planes are consumed). */
+size_t tdec_planes_bytes(const tdec_t *h, int B);
+int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, float *d_planes, void *stream);
+int tdec_decode_planes_dev(tdec_t *h, int B, float *d_planes, int32_t *d_bits, double *d_lfinal,
+                           void *stream);
+int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits,
+                          double *d_lfinal, void *stream);
+
+/* Soft demapper: compute_llr (test_sdr_with_coding.py:200-225) over any
+ * labelled constellation (label i = bits MSB first).  syms: n_sym complex
+ * values (f32 pairs, or f64 pairs when sym_f64); cons: M points (host memory,
+ * f32 or f64 pairs).  Arithmetic dtype = f64 if either is f64.  div_f32: the
+ * (min_d0 - min_d1) / noise_var division stays float32 (numpy >= 2 with a
+ * Python-float noise_var).  sign = +1 reference sign (positive -> bit 1),
+ * -1 decoder sign.  Output f64[n_sym * bps]. */
+int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, const void *cons, int cons_f64,
+                   int M, int bps, double noise_var, int div_f32, int sign, double *d_llr, void *stream);
+int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M,
+               int bps, double noise_var, int div_f32, int sign, double *llr);
+
+/* Fused demap -> de-puncture for the decoder: B codewords of S complex64
+ * symbols each ([B][S]); LLR j of a codeword = bit j of its symbol stream
+ * (zero-padded / truncated to the decoder's LLR count as
+ * test_sdr_with_coding.py:474-478), decoder sign, rounded to f32 as decode()
+ * does (:466).  Writes the plane buffer consumed by tdec_decode_planes_dev. */
+int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
+                          int bps, double noise_var, int div_f32, float *d_planes, void *stream);
+
+/* Batched encoder (workload generation): encode (dvb_rcs2_turbo.py:404-462)
+ * with the handle's perm, bits uint8[B][2N] -> coded uint8[B][n_out],
+ * n_out = the reference encoder's output length. */
+int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream);
+long tdec_encoded_len(const tdec_t *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDEC_H */

@@ -1,0 +1,114 @@
+"""ctypes binding of the gfx950 HIP library (modulations_amd/lib/libtdec.so).
+
+The product path has no CPU fallback: if the library is missing or no HIP
+device is visible, calls raise instead of computing anything on the host.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtdec.so")
+
+TDEC_OK, TDEC_EINVAL, TDEC_ESHORT, TDEC_ENOMEM, TDEC_EHIP, TDEC_EUNSUPPORTED, TDEC_EITER, TDEC_ECAPACITY = \
+    0, -1, -2, -3, -4, -5, -6, -7
+
+# every symbol include/tdec.h declares (tests check the library exports them all)
+EXPORTS = (
+    "tdec_create", "tdec_destroy", "tdec_last_error", "tdec_llr_len", "tdec_siso_batch", "tdec_decode_batch",
+    "tdec_reserve", "tdec_planes_bytes", "tdec_depuncture_dev", "tdec_decode_planes_dev", "tdec_decode_batch_dev",
+    "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
+)
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = C.c_void_p
+
+
+def _declare(L):
+    L.tdec_create.argtypes = [C.c_int, C.c_int, C.c_int, _vp, C.c_int, C.c_int, _vp, _vp, _vp, C.POINTER(_vp)]
+    L.tdec_create.restype = C.c_int
+    L.tdec_destroy.argtypes = [_vp]
+    L.tdec_destroy.restype = None
+    L.tdec_last_error.argtypes = []
+    L.tdec_last_error.restype = C.c_char_p
+    L.tdec_llr_len.argtypes = [_vp]
+    L.tdec_llr_len.restype = C.c_long
+    L.tdec_encoded_len.argtypes = [_vp]
+    L.tdec_encoded_len.restype = C.c_long
+    L.tdec_siso_batch.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_double, _vp, _vp]
+    L.tdec_decode_batch.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
+    L.tdec_reserve.argtypes = [_vp, C.c_int]
+    L.tdec_planes_bytes.argtypes = [_vp, C.c_int]
+    L.tdec_planes_bytes.restype = C.c_size_t
+    L.tdec_depuncture_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
+    L.tdec_decode_planes_dev.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp]
+    L.tdec_decode_batch_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp, _vp]
+    L.tdec_demap_dev.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
+                                 C.c_int, C.c_int, _vp, _vp]
+    L.tdec_demap.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
+                             C.c_int, C.c_int, _vp]
+    L.tdec_demap_planes_dev.argtypes = [_vp, C.c_int, _vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
+                                        C.c_int, _vp, _vp]
+    L.tdec_encode_dev.argtypes = [_vp, C.c_int, _vp, _vp, _vp]
+    for name in EXPORTS:
+        f = getattr(L, name)
+        if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",
+                                            "tdec_depuncture_dev", "tdec_decode_planes_dev",
+                                            "tdec_decode_batch_dev", "tdec_demap_dev", "tdec_demap",
+                                            "tdec_demap_planes_dev", "tdec_encode_dev"):
+            f.restype = C.c_int
+
+
+def lib():
+    """Load libtdec.so (building it first if this is a build tree without it)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    from . import build
+                    build.build()
+                L = C.CDLL(LIB_PATH)
+                _declare(L)
+                _lib = L
+    return _lib
+
+
+class TdecError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc == TDEC_OK:
+        return
+    msg = lib().tdec_last_error().decode(errors="replace")
+    if rc == TDEC_EINVAL or rc == TDEC_EUNSUPPORTED:
+        raise ValueError(msg)
+    if rc == TDEC_ESHORT:
+        raise IndexError(msg)
+    if rc == TDEC_ENOMEM:
+        raise MemoryError(msg)
+    if rc == TDEC_EITER:
+        raise UnboundLocalError(msg)
+    raise TdecError(f"tdec error {rc}: {msg}")
+
+
+def ptr(a):
+    """Device or host address of a numpy array / torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+def stream_ptr(stream):
+    if stream is None:
+        return None
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)

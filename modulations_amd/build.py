@@ -1,0 +1,42 @@
+"""Build the gfx950 HIP library (modulations_amd/lib/libtdec.so) in-tree.
+
+``python -m modulations_amd.build`` or ``modulations_amd.build.build()``.
+hipcc cross-compiles for gfx950 without a GPU.  Flags that the numerics need:
+  -ffp-contract=off                  no FMA contraction (the reference has none)
+  -fno-gpu-flush-denormals-to-zero   IEEE f32 denormals, as numpy/numba
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "tdec_api.hip")
+DEPS = [SRC, os.path.join(HERE, "csrc", "tdec_kernels.hip"), os.path.join(ROOT, "include", "tdec.h")]
+OUT = os.path.join(HERE, "lib", "libtdec.so")
+
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-fno-gpu-flush-denormals-to-zero", "-Wall", "-Wno-unused-value", "-Wno-unused-result"]
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    return "hipcc"
+
+
+def build(force=False, extra=()):
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
+        return OUT
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", OUT, SRC]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("hipcc failed building libtdec.so")
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

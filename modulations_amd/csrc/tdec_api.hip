@@ -1,0 +1,508 @@
+// tdec_api.hip -- the C ABI (include/tdec.h) over the gfx950 kernels.
+//
+// Host-pointer entry points stage through handle-owned, grow-only device
+// buffers and synchronise; _dev entry points are stream-ordered, allocation
+// free once tdec_reserve() has sized the workspace (hipGraph-capturable).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tdec.h"
+#include "tdec_kernels.hip"
+
+using namespace tdec;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? TDEC_ENOMEM : TDEC_EHIP,                  \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) return fail(TDEC_ENOMEM, "hipMalloc failed");
+        cap = bytes;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Guard {  // select the handle's device for the duration of a call
+    int prev = -1;
+    explicit Guard(int dev) {
+        hipGetDevice(&prev);
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~Guard() {
+        int cur;
+        hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) hipSetDevice(prev);
+    }
+};
+
+bool standard_trellis(const int32_t *t) {
+    for (int s = 0; s < 16; ++s)
+        for (int i = 0; i < 4; ++i) {
+            if (t[0 * 64 + s * 4 + i] != t_next(s, i)) return false;
+            if (t[1 * 64 + s * 4 + i] != t_ow(s, i)) return false;
+            if (t[2 * 64 + s * 4 + i] != t_oy(s, i)) return false;
+            if (t[3 * 64 + s * 4 + i] != t_prev_s(s, i)) return false;
+            if (t[4 * 64 + s * 4 + i] != t_prev_i(s, i)) return false;
+        }
+    return true;
+}
+
+// GF(2) circular-state solve of the encoder (dvb_rcs2_turbo.py:37-114).
+void mat_mul_gf2(const int *A, const int *B, int *C) {
+    int T[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            int v = 0;
+            for (int k = 0; k < 4; ++k) v ^= A[i * 4 + k] & B[k * 4 + j];
+            T[i * 4 + j] = v;
+        }
+    std::memcpy(C, T, sizeof T);
+}
+
+int solve_circ(const int *Gp, int Z) {
+    int M[4][5];
+    for (int i = 0; i < 4; ++i) {
+        for (int j = 0; j < 4; ++j) M[i][j] = ((i == j) + Gp[i * 4 + j]) % 2;
+        M[i][4] = (Z >> i) & 1;
+    }
+    for (int i = 0; i < 4; ++i) {
+        if (M[i][i] == 0)
+            for (int k = i + 1; k < 4; ++k)
+                if (M[k][i] == 1) {
+                    for (int j = 0; j < 5; ++j) std::swap(M[i][j], M[k][j]);
+                    break;
+                }
+        if (M[i][i] == 1)
+            for (int k = i + 1; k < 4; ++k)
+                if (M[k][i] == 1)
+                    for (int j = 0; j < 5; ++j) M[k][j] ^= M[i][j];
+    }
+    int x[4] = {0, 0, 0, 0};
+    for (int i = 3; i >= 0; --i) {
+        int s = M[i][4];
+        for (int j = i + 1; j < 4; ++j) s ^= M[i][j] & x[j];
+        x[i] = s;
+    }
+    int st = 0;
+    for (int i = 0; i < 4; ++i)
+        if (x[i]) st |= 1 << i;
+    return st;
+}
+
+// Constellation table to device memory, in the arithmetic dtype.  The upload
+// synchronises once; later calls with the same table find it cached and stay
+// fully stream-ordered.
+struct ConsCache {
+    DevBuf buf;
+    std::vector<double> host;
+    bool f64 = false;
+    int upload(const void *cons, int cons_f64, int M, bool want_f64, hipStream_t st) {
+        std::vector<double> d(2 * M);
+        for (int i = 0; i < 2 * M; ++i)
+            d[i] = cons_f64 ? ((const double *)cons)[i] : (double)((const float *)cons)[i];
+        if (buf.p && d == host && f64 == want_f64) return 0;
+        if (int rc = buf.ensure(sizeof(double) * 512)) return rc;
+        std::vector<float> f(d.begin(), d.end());   // exact: an f32 table only meets f32 arithmetic
+        if (want_f64) HIPCHK(hipMemcpyAsync(buf.p, d.data(), sizeof(double) * 2 * M, hipMemcpyHostToDevice, st));
+        else HIPCHK(hipMemcpyAsync(buf.p, f.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        host = d;
+        f64 = want_f64;
+        return 0;
+    }
+};
+
+// ---- demapper -------------------------------------------------------------------------
+template <typename T, typename S>
+int launch_demap(int bps, const S *d_syms, long n_sym, const T *d_cons, DemapCfg c, double *d_llr,
+                        hipStream_t st) {
+    const dim3 grid((unsigned)((n_sym + BLOCK - 1) / BLOCK));
+    switch (bps) {
+#define CASE(K) \
+    case K: hipLaunchKernelGGL((k_demap<T, S, K>), grid, dim3(BLOCK), 0, st, d_syms, n_sym, d_cons, c, d_llr); break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default: return fail(TDEC_EINVAL, "bps must be 1..8");
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int check_demap_args(int M, int bps) {
+    if (bps < 1 || bps > 8 || M < 1 || M > (1 << bps) || M > 256) return fail(TDEC_EINVAL, "bad constellation size");
+    return 0;
+}
+
+}  // namespace
+
+struct tdec_ctx {
+    int device = 0, N = 0, period = 1, iters = 8, algo = 0;
+    uint8_t punct[16] = {0};
+    long llr_len = 0, enc_len = 0;
+    bool needs_zero = false;           // punctured positions exist (planes must be zero-filled)
+    int circ[16] = {0};
+    int max_waves = 0;                 // resident waves of the decode kernel on this device
+    int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_dst = nullptr;
+    DevBuf le, ck;                     // per-wave decode workspace
+    int ws_waves = 0;
+    DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
+    int cap_batch = 0;
+    DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
+    ConsCache cons;                    // demapper constellation
+    hipStream_t stream = nullptr;
+};
+
+extern "C" {
+
+const char *tdec_last_error(void) { return g_err.c_str(); }
+
+int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int iterations, int algo,
+                const int32_t *perm, const int32_t *inv_perm, const int32_t *tables, tdec_t **out) {
+    if (!out || !punct || !perm || !inv_perm || !tables) return fail(TDEC_EINVAL, "null argument");
+    *out = nullptr;
+    if (n_couples <= 0 || n_couples % WIN) return fail(TDEC_EINVAL, "n_couples must be a positive multiple of 4");
+    if (period < 1 || period > 4) return fail(TDEC_EINVAL, "puncture period must be 1..4");
+    if (iterations < 1) return fail(TDEC_EITER, "iterations must be >= 1");
+    if (algo != TDEC_ALGO_MAXLOG && algo != TDEC_ALGO_LOGMAP) return fail(TDEC_EINVAL, "unknown algorithm");
+    if (!standard_trellis(tables))
+        return fail(TDEC_EUNSUPPORTED, "trellis tables are not the DVB-RCS2 16-state CRSC trellis");
+    for (int k = 0; k < n_couples; ++k)
+        if (perm[k] < 0 || perm[k] >= n_couples || inv_perm[k] < 0 || inv_perm[k] >= n_couples)
+            return fail(TDEC_EINVAL, "perm / inv_perm entry out of range");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(TDEC_EHIP, "no such HIP device");
+    Guard g(device);
+    auto *h = new tdec_ctx;
+    h->device = device;
+    h->N = n_couples;
+    h->period = period;
+    h->iters = iterations;
+    h->algo = algo;
+    std::memcpy(h->punct, punct, 16);
+    const int N = n_couples;
+    // de-puncture walk (:476-487) -> src[c*N + k] (LLR index or -1) for the 8 float4
+    // components of the tile planes (X = A, B, W1, Y1; Z = -, -, W2, Y2) and its inverse
+    std::vector<int32_t> src(8 * (size_t)N, -1);
+    long idx = 0;
+    static const int comp_of_row[4] = {2, 3, 6, 7};   // W1 -> X.z, Y1 -> X.w, W2 -> Z.z, Y2 -> Z.w
+    for (int i = 0; i < N; ++i) {
+        const int p = i % period;
+        src[0 * (size_t)N + i] = (int32_t)idx++;
+        src[1 * (size_t)N + i] = (int32_t)idx++;
+        for (int r = 0; r < 4; ++r) {
+            if (punct[r * 4 + p]) src[comp_of_row[r] * (size_t)N + i] = (int32_t)idx++;
+            else h->needs_zero = true;
+        }
+    }
+    h->llr_len = idx;
+    h->enc_len = idx;   // encode() writes exactly what decode() reads (:449-460)
+    std::vector<int32_t> dst(idx);
+    for (int c = 0; c < 8; ++c)
+        for (int k = 0; k < N; ++k) {
+            const int j = src[(size_t)c * N + k];
+            if (j >= 0) dst[j] = (int32_t)(((c / 4) * N + k) * 4 + (c % 4));
+        }
+    // encoder circular-state table: S_c = solve((I + G^N), Z) for every Z (:414-417)
+    int G[16] = {0};
+    G[0 * 4 + 2] = G[0 * 4 + 3] = G[1 * 4 + 0] = G[2 * 4 + 1] = G[3 * 4 + 2] = 1;
+    int res[16], base[16];
+    for (int i = 0; i < 16; ++i) res[i] = (i % 5) == 0;
+    std::memcpy(base, G, sizeof base);
+    for (long pw = N; pw > 0; pw /= 2) {
+        if (pw % 2 == 1) mat_mul_gf2(res, base, res);
+        mat_mul_gf2(base, base, base);
+    }
+    for (int z = 0; z < 16; ++z) h->circ[z] = solve_circ(res, z);
+
+    hipError_t e = hipSuccess;
+    e = hipMalloc(&h->d_perm, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
+    if (e == hipSuccess) e = hipMalloc(&h->d_dst, sizeof(int32_t) * std::max<long>(idx, 1));
+    if (e == hipSuccess) e = hipMemcpy(h->d_perm, perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->d_inv, inv_perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->d_src, src.data(), sizeof(int32_t) * 8 * N, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->d_dst, dst.data(), sizeof(int32_t) * idx, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    int blocks_per_cu = 0, n_cu = 0;
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks_per_cu, algo ? (const void *)k_turbo_decode<1> : (const void *)k_turbo_decode<0>, BLOCK, 0);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) {
+        tdec_destroy(h);
+        return fail(TDEC_EHIP, std::string("tdec_create: ") + hipGetErrorString(e));
+    }
+    h->max_waves = std::max(1, blocks_per_cu) * n_cu * WAVES_PER_BLOCK;
+    *out = h;
+    return TDEC_OK;
+}
+
+void tdec_destroy(tdec_t *h) {
+    if (!h) return;
+    Guard g(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    hipFree(h->d_perm);
+    hipFree(h->d_inv);
+    hipFree(h->d_src);
+    hipFree(h->d_dst);
+    h->le.release();
+    h->ck.release();
+    h->planes_own.release();
+    h->h_llr.release();
+    h->h_bits.release();
+    h->h_lf.release();
+    h->h_misc.release();
+    h->cons.buf.release();
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+}
+
+long tdec_llr_len(const tdec_t *h) { return h ? h->llr_len : TDEC_EINVAL; }
+long tdec_encoded_len(const tdec_t *h) { return h ? h->enc_len : TDEC_EINVAL; }
+
+size_t tdec_planes_bytes(const tdec_t *h, int B) {
+    if (!h || B <= 0) return 0;
+    const size_t tiles = ((size_t)B + WAVE - 1) / WAVE;
+    return tiles * 2 * (size_t)h->N * WAVE * sizeof(float4);
+}
+
+static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
+
+// Workspace for `waves` concurrently decoding waves.
+static int ensure_ws(tdec_t *h, int waves) {
+    if (waves <= h->ws_waves) return 0;
+    const size_t N = h->N;
+    int rc = h->le.ensure((size_t)waves * 2 * N * WAVE * sizeof(double2));
+    if (!rc) rc = h->ck.ensure((size_t)waves * (N / WIN) * 4 * WAVE * sizeof(float4));
+    if (rc) return rc;
+    h->ws_waves = waves;
+    return 0;
+}
+
+int tdec_reserve(tdec_t *h, int max_batch) {
+    if (!h || max_batch <= 0) return fail(TDEC_EINVAL, "bad reserve");
+    Guard g(h->device);
+    int rc = ensure_ws(h, std::min(n_tiles_of(max_batch), h->max_waves));
+    if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
+    if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
+    return rc;
+}
+
+int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, float *d_planes, void *stream) {
+    if (!h || !d_llr || !d_planes || B <= 0) return fail(TDEC_EINVAL, "bad depuncture arguments");
+    if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
+    Guard g(h->device);
+    const long total = (long)n_tiles_of(B) * 2 * h->N * WAVE;
+    hipLaunchKernelGGL(k_depuncture, dim3((unsigned)((total + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                       (hipStream_t)stream, B, h->N, d_llr, llr_stride, (const int *)h->d_src, (float4 *)d_planes,
+                       total);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdec_decode_planes_dev(tdec_t *h, int B, float *d_planes, int32_t *d_bits, double *d_lfinal,
+                           void *stream) {
+    if (!h || !d_planes || !d_bits || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    Guard g(h->device);
+    const int tiles = n_tiles_of(B);
+    const int waves = std::min(tiles, h->max_waves);
+    if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, (float4 *)d_planes,
+                 (double2 *)h->le.p, (float4 *)h->ck.p, d_bits, d_lfinal};
+    const int *pm = h->d_perm, *iv = h->d_inv;
+    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (h->algo) hipLaunchKernelGGL(k_turbo_decode<1>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a, pm, iv);
+    else hipLaunchKernelGGL(k_turbo_decode<0>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a, pm, iv);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits, double *d_lfinal,
+                          void *stream) {
+    if (!h || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (B > h->cap_batch) return fail(TDEC_ECAPACITY, "batch larger than tdec_reserve()");
+    int rc = tdec_depuncture_dev(h, B, d_llr, llr_stride, (float *)h->planes_own.p, stream);
+    if (!rc) rc = tdec_decode_planes_dev(h, B, (float *)h->planes_own.p, d_bits, d_lfinal, stream);
+    return rc;
+}
+
+int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32_t *bits, double *lfinal) {
+    if (!h || !llr || !bits || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
+    Guard g(h->device);
+    int rc = tdec_reserve(h, B);
+    const size_t nl = (size_t)B * llr_stride * sizeof(float), nb = (size_t)B * 2 * h->N;
+    if (!rc) rc = h->h_llr.ensure(nl);
+    if (!rc) rc = h->h_bits.ensure(nb * sizeof(int32_t));
+    if (!rc && lfinal) rc = h->h_lf.ensure(nb * sizeof(double));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h->h_llr.p, llr, nl, hipMemcpyHostToDevice, h->stream));
+    rc = tdec_decode_batch_dev(h, B, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
+                               lfinal ? (double *)h->h_lf.p : nullptr, h->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(bits, h->h_bits.p, nb * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+    if (lfinal) HIPCHK(hipMemcpyAsync(lfinal, h->h_lf.p, nb * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
+                    const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {
+    if (!h || B <= 0 || !LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB)
+        return fail(TDEC_EINVAL, "bad siso arguments");
+    Guard g(h->device);
+    const int waves = n_tiles_of(B);
+    const size_t N = h->N, nf = (size_t)B * N * sizeof(float), nd = (size_t)B * N * sizeof(double);
+    int rc = ensure_ws(h, waves);
+    if (!rc) rc = h->h_misc.ensure(4 * nf + 4 * nd);
+    if (rc) return rc;
+    char *base = (char *)h->h_misc.p;
+    float *dA = (float *)base, *dB = (float *)(base + nf), *dW = (float *)(base + 2 * nf), *dY = (float *)(base + 3 * nf);
+    double *daA = (double *)(base + 4 * nf), *daB = (double *)(base + 4 * nf + nd);
+    double *deA = (double *)(base + 4 * nf + 2 * nd), *deB = (double *)(base + 4 * nf + 3 * nd);
+    hipStream_t s = h->stream;
+    HIPCHK(hipMemcpyAsync(dA, LcA, nf, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dB, LcB, nf, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dW, LcW, nf, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dY, LcY, nf, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(daA, LaA, nd, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
+    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p};
+    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (h->algo) hipLaunchKernelGGL(k_siso_batch<1>, grid, dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL(k_siso_batch<0>, grid, dim3(BLOCK), 0, s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(LeA, deA, nd, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(LeB, deB, nd, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M,
+                   int bps, double noise_var, int div_f32, int sign, double *d_llr, void *stream) {
+    if (!d_syms || !cons || !d_llr || n_sym < 0) return fail(TDEC_EINVAL, "bad demap arguments");
+    if (int rc = check_demap_args(M, bps)) return rc;
+    if (n_sym == 0) return 0;
+    Guard g(device);
+    static thread_local ConsCache tbl[16];
+    ConsCache &cc = tbl[device & 15];
+    const bool f64 = sym_f64 || cons_f64;
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = cc.upload(cons, cons_f64, M, f64, st)) return rc;
+    DevBuf &tb = cc.buf;
+    DemapCfg c{M, div_f32, sign, (0.005 > noise_var) ? 0.005 : noise_var};
+    if (f64) {
+        if (sym_f64) return launch_demap<double, double>(bps, (const double *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
+        return launch_demap<double, float>(bps, (const float *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
+    }
+    return launch_demap<float, float>(bps, (const float *)d_syms, n_sym, (const float *)tb.p, c, d_llr, st);
+}
+
+int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M, int bps,
+               double noise_var, int div_f32, int sign, double *llr) {
+    if (!syms || !cons || !llr || n_sym < 0) return fail(TDEC_EINVAL, "bad demap arguments");
+    if (int rc = check_demap_args(M, bps)) return rc;
+    if (n_sym == 0) return 0;
+    Guard g(device);
+    const size_t ns = (size_t)n_sym * 2 * (sym_f64 ? 8 : 4), nl = (size_t)n_sym * bps * sizeof(double);
+    void *ds = nullptr, *dl = nullptr;
+    HIPCHK(hipMalloc(&ds, ns));
+    if (hipMalloc(&dl, nl) != hipSuccess) {
+        hipFree(ds);
+        return fail(TDEC_ENOMEM, "hipMalloc failed");
+    }
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    int rc = 0;
+    if (hipMemcpyAsync(ds, syms, ns, hipMemcpyHostToDevice, st) != hipSuccess) rc = fail(TDEC_EHIP, "memcpy");
+    if (!rc) rc = tdec_demap_dev(device, ds, sym_f64, n_sym, cons, cons_f64, M, bps, noise_var, div_f32, sign,
+                                 (double *)dl, st);
+    if (!rc && hipMemcpyAsync(llr, dl, nl, hipMemcpyDeviceToHost, st) != hipSuccess) rc = fail(TDEC_EHIP, "memcpy");
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = fail(TDEC_EHIP, "demap failed");
+    hipStreamDestroy(st);
+    hipFree(ds);
+    hipFree(dl);
+    return rc;
+}
+
+int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
+                          int bps, double noise_var, int div_f32, float *d_planes, void *stream) {
+    if (!h || !d_syms || !cons || !d_planes || B <= 0 || S <= 0) return fail(TDEC_EINVAL, "bad demap arguments");
+    if (int rc = check_demap_args(M, bps)) return rc;
+    Guard g(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = h->cons.upload(cons, cons_f64, M, cons_f64 != 0, st)) return rc;
+    if (h->needs_zero || (long)S * bps < h->llr_len)   // punctured / missing LLRs stay 0.0 (:469-474, :474-476)
+        HIPCHK(hipMemsetAsync(d_planes, 0, tdec_planes_bytes(h, B), st));
+    DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var};
+    const long total = (long)n_tiles_of(B) * WAVE * S;
+    const dim3 grid((unsigned)((total + BLOCK - 1) / BLOCK));
+    switch (bps) {
+#define CASE(K)                                                                                              \
+    case K:                                                                                                  \
+        if (cons_f64)                                                                                        \
+            hipLaunchKernelGGL((k_demap_planes<double, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,     \
+                               (const double *)h->cons.buf.p, c, (const int *)h->d_dst, h->llr_len, d_planes);  \
+        else                                                                                                 \
+            hipLaunchKernelGGL((k_demap_planes<float, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,      \
+                               (const float *)h->cons.buf.p, c, (const int *)h->d_dst, h->llr_len, d_planes);   \
+        break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default: return fail(TDEC_EINVAL, "bps must be 1..8");
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream) {
+    if (!h || !d_bits || !d_coded || B <= 0) return fail(TDEC_EINVAL, "bad encode arguments");
+    Guard g(h->device);
+    EncodeArgs a{};
+    a.B = B;
+    a.N = h->N;
+    a.period = h->period;
+    a.n_out = h->enc_len;
+    std::memcpy(a.punct, h->punct, 16);
+    std::memcpy(a.circ, h->circ, sizeof a.circ);
+    a.perm = h->d_perm;
+    a.bits = d_bits;
+    a.coded = d_coded;
+    hipLaunchKernelGGL(k_encode, dim3((B + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, (hipStream_t)stream, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

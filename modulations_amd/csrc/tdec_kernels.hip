@@ -1,0 +1,571 @@
+// tdec_kernels.hip -- gfx950 kernels of the DVB-RCS2 duo-binary turbo decoder.
+//
+// Design: one codeword per LANE.  The 16-state trellis is a
+// compile-time constant, so a wave advances 64 independent codewords through
+// the alpha/beta recursions with every state metric in VGPRs and no cross-lane
+// traffic at all (no shuffles, no LDS).  Per-codeword streams live in HBM in a
+// "tile" layout [tile][plane][k][64 lanes]: a wave's load of one trellis step
+// is one contiguous 256 B (f32) or 512 B (f64) segment, and the interleaver
+// gathers (perm[k] is the same for every codeword) stay coalesced.
+//
+// Numerics restate dvb_rcs2_turbo.py:116-281 operation for operation:
+//   gamma: f64 sum (((±A ± B) ± W) ± Y)/2 rounded once to f32      (:127-160)
+//   alpha/beta: f32 add, running max from -1e9, subtract state 0   (:162-230)
+//   extrinsic: (alpha + gamma) + beta in f32, max_star, f64 tail   (:232-281)
+// Compiled with -ffp-contract=off (no FMA contraction) and IEEE denormals.
+// fmaxf chains are value-identical to the reference's `if t > m: m = t`
+// (maxNum drops a NaN operand exactly as the strict compare does; only the
+// sign of an exact zero can differ, which compares equal everywhere).
+//
+// The alpha metrics of the second forward pass are not stored: every W-th
+// vector is checkpointed and the window is recomputed (bit-exact, the same
+// operations) during the final backward pass, which fuses beta and the
+// extrinsic.  HBM traffic per SISO is therefore ~4 reads of the branch inputs
+// + the extrinsic write + the checkpoints.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdec {
+
+constexpr int NS = 16;
+constexpr int WAVE = 64;
+constexpr float NEG = -1.0e9f;   // NEG_INF_VAL of :125, exact in f32
+
+// ---- trellis of _init_trellis (:327-396), as constexpr bit formulas -------
+__host__ __device__ constexpr int sb(int s, int i) { return (s >> i) & 1; }
+__host__ __device__ constexpr int t_dk(int s, int inp) { return ((inp >> 1) & 1) ^ (inp & 1) ^ sb(s, 2) ^ sb(s, 3); }
+__host__ __device__ constexpr int t_next(int s, int inp) {
+    return (sb(s, 2) << 3) | (sb(s, 1) << 2) | (sb(s, 0) << 1) | t_dk(s, inp);
+}
+__host__ __device__ constexpr int t_ow(int s, int inp) { return t_dk(s, inp) ^ sb(s, 0) ^ sb(s, 1) ^ sb(s, 3); }
+__host__ __device__ constexpr int t_oy(int s, int inp) { return t_dk(s, inp) ^ sb(s, 1) ^ sb(s, 2) ^ sb(s, 3); }
+// prev_state / prev_input in the order the reference's scan fills them
+__host__ __device__ constexpr int t_prev_s(int ns, int idx) { return ((ns >> 1) & 7) | ((idx >> 1) << 3); }
+__host__ __device__ constexpr int t_prev_i(int ns, int idx) {
+    return ((ns & 1) ^ sb(t_prev_s(ns, idx), 2) ^ sb(t_prev_s(ns, idx), 3)) ? ((idx & 1) ? 2 : 1)
+                                                                           : ((idx & 1) ? 3 : 0);
+}
+
+// ---- branch metrics ---------------------------------------------------------
+// Only 16 distinct values per step: g(bA,bB,bW,bY).  g(~bits) = -g(bits)
+// exactly (round-to-nearest is sign-symmetric), so 8 are stored: index
+// bB*4 + bW*2 + bY with bA = 0.
+__device__ __forceinline__ void make_gamma(float a, float b, double laA, double laB, float w, float y,
+                                           float (&g)[8], double &inA, double &inB) {
+    inA = (double)a + laA;
+    inB = (double)b + laB;
+    const double hA = inA * 0.5, hB = inB * 0.5, hW = (double)w * 0.5, hY = (double)y * 0.5;
+    const double l1[2] = {hA + hB, hA + (-hB)};
+#pragma unroll
+    for (int bB = 0; bB < 2; ++bB)
+#pragma unroll
+        for (int bW = 0; bW < 2; ++bW) {
+            const double l2 = l1[bB] + (bW ? -hW : hW);
+            g[bB * 4 + bW * 2 + 0] = (float)(l2 + hY);
+            g[bB * 4 + bW * 2 + 1] = (float)(l2 + (-hY));
+        }
+}
+
+__device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
+    const int bA = (inp >> 1) & 1, bB = inp & 1, bW = t_ow(s, inp), bY = t_oy(s, inp);
+    return bA == 0 ? g[bB * 4 + bW * 2 + bY] : -g[(bB ^ 1) * 4 + (bW ^ 1) * 2 + (bY ^ 1)];
+}
+
+// ---- max / max* ---------------------------------------------------------------
+// log-MAP (build-defined): Jacobian log with the historic 37 cut-off.
+__device__ __forceinline__ float jac(float a, float b) {
+    const float m = a > b ? a : b;
+    const float d = fabsf(a - b);
+    const float c = log1pf(expf(-d));
+    return (d <= 37.0f) ? m + c : m;     // NaN d and d > 37 keep m
+}
+
+template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {
+    if constexpr (ALGO == 0) return fmaxf(m, t);
+    else return jac(m, t);
+}
+
+template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   // max_star, :32-35
+    if constexpr (ALGO == 0) return a > b ? a : b;
+    else return jac(a, b);
+}
+
+// ---- recursions -----------------------------------------------------------------
+template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], const float (&g)[8]) {
+    float na[NS];
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) {
+        float m = NEG;
+#pragma unroll
+        for (int idx = 0; idx < 4; ++idx) {
+            const int ps = t_prev_s(ns, idx), in = t_prev_i(ns, idx);
+            m = acc<ALGO>(m, a[ps] + gam(g, ps, in));
+        }
+        na[ns] = m;
+    }
+    const float norm = na[0];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) a[s] = na[s] - norm;
+}
+
+template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], const float (&g)[8]) {
+    float nb[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        float m = NEG;
+#pragma unroll
+        for (int inp = 0; inp < 4; ++inp) m = acc<ALGO>(m, b[t_next(s, inp)] + gam(g, s, inp));
+        nb[s] = m;
+    }
+    const float norm = nb[0];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
+}
+
+template <int ALGO>
+__device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)[8], const float (&b1)[NS], double inA,
+                                          double inB, double sf, double &leA, double &leB) {
+    float app[4] = {NEG, NEG, NEG, NEG};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int inp = 0; inp < 4; ++inp) app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
+    const float pA0 = star<ALGO>(app[0], app[1]), pA1 = star<ALGO>(app[2], app[3]);
+    const float pB0 = star<ALGO>(app[0], app[2]), pB1 = star<ALGO>(app[1], app[3]);
+    const float LpA = pA0 - pA1, LpB = pB0 - pB1;
+    double x = ((double)LpA - inA) * sf;
+    double y = ((double)LpB - inB) * sf;
+    x = x > 300.0 ? 300.0 : x;
+    x = x < -300.0 ? -300.0 : x;
+    y = y > 300.0 ? 300.0 : y;
+    y = y < -300.0 ? -300.0 : y;
+    leA = x;
+    leB = y;
+}
+
+// ---- per-lane SISO --------------------------------------------------------------
+// Raw branch inputs of one trellis step: {Lc_A, Lc_B, Lc_W, Lc_Y} (f32) and the
+// a-priori {La_A, La_B} (f64).  32 B per lane, two 16-B loads.
+struct Raw {
+    float4 v;
+    double2 l;
+};
+
+__device__ __forceinline__ void gamma_of(const Raw &r, float (&g)[8], double &iA, double &iB) {
+    make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+}
+
+// Branch inputs of one component decoder in the tile layout: X = [N][64] float4
+// (uniform base), La = [N][64] double2 gathered through la_idx (perm / inv_perm,
+// the same index for every lane), or null for the all-zero a-priori of the
+// first iteration (:490-491).
+struct TileIn {
+    const float4 *X;
+    const double2 *La;
+    const int *la_idx;
+    int lane;
+    __device__ __forceinline__ Raw load(int k) const {
+        Raw r;
+        r.v = X[(long)k * WAVE + lane];
+        if (La) {
+            const long kl = la_idx ? la_idx[k] : k;
+            r.l = La[kl * WAVE + lane];
+        } else {
+            r.l = make_double2(0.0, 0.0);
+        }
+        return r;
+    }
+};
+
+struct TileOut {
+    double2 *Le;
+    int lane;
+    __device__ __forceinline__ void store(int k, double a, double b) const { Le[(long)k * WAVE + lane] = make_double2(a, b); }
+};
+
+// [B][N] row layout of the bcjr_max_log_map boundary (one codeword per lane).
+struct RowIn {
+    const float *A, *B, *W, *Y;
+    const double *LaA, *LaB;
+    __device__ __forceinline__ Raw load(int k) const {
+        Raw r;
+        r.v = make_float4(A[k], B[k], W[k], Y[k]);
+        r.l = make_double2(LaA[k], LaB[k]);
+        return r;
+    }
+};
+
+struct RowOut {
+    double *A, *B;
+    bool active;
+    __device__ __forceinline__ void store(int k, double a, double b) const {
+        if (active) {
+            A[k] = a;
+            B[k] = b;
+        }
+    }
+};
+
+// bcjr_max_log_map (:116-281) for the calling lane's codeword.
+// ck: checkpoint ring of this wave, [(N/W)][4][64] float4 (uniform base).
+// Inputs are software-pipelined one group of W steps ahead.
+template <int ALGO, int W, class In, class Out>
+__device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, double sf) {
+    Raw cur[W], nxt[W];
+    float a[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) a[s] = 0.0f;
+    // forward pass 1 (convergence, :165-179) and pass 2 (:186-197) after alpha[0] = alpha[N]
+    // (:182-183); pass 2 checkpoints alpha every W steps.
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) cur[j] = in.load(j);
+        for (int k0 = 0; k0 < N; k0 += W) {
+            if (k0 + W < N) {
+#pragma unroll
+                for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 + W + j);
+            }
+            if (pass) {
+                float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c[q * WAVE] = make_float4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+            }
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                float g[8];
+                double iA, iB;
+                gamma_of(cur[j], g, iA, iB);
+                alpha_step<ALGO>(a, g);
+            }
+#pragma unroll
+            for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+        }
+    }
+    // backward pass 1 (:203-213)
+    float b[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[s] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < W; ++j) cur[j] = in.load(N - W + j);
+    for (int k0 = N - W; k0 >= 0; k0 -= W) {
+        if (k0 > 0) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 - W + j);
+        }
+#pragma unroll
+        for (int j = W - 1; j >= 0; --j) {
+            float g[8];
+            double iA, iB;
+            gamma_of(cur[j], g, iA, iB);
+            beta_step<ALGO>(b, g);
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+    }
+    // beta[N] = beta[0] (:216-217); backward pass 2 fused with the extrinsic
+    // (:220-281), alpha recomputed per window from its checkpoint.
+#pragma unroll
+    for (int j = 0; j < W; ++j) cur[j] = in.load(N - W + j);
+    for (int k0 = N - W; k0 >= 0; k0 -= W) {
+        if (k0 > 0) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 - W + j);
+        }
+        float aw[W][NS], gw[W][8];
+        double iAw[W], iBw[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) gamma_of(cur[j], gw[j], iAw[j], iBw[j]);
+        const float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = c[q * WAVE];
+            aw[0][4 * q] = v.x;
+            aw[0][4 * q + 1] = v.y;
+            aw[0][4 * q + 2] = v.z;
+            aw[0][4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int j = 1; j < W; ++j) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) aw[j][s] = aw[j - 1][s];
+            alpha_step<ALGO>(aw[j], gw[j - 1]);
+        }
+#pragma unroll
+        for (int j = W - 1; j >= 0; --j) {
+            double leA, leB;
+            extrinsic<ALGO>(aw[j], gw[j], b, iAw[j], iBw[j], sf, leA, leB);
+            out.store(k0 + j, leA, leB);
+            beta_step<ALGO>(b, gw[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+    }
+}
+
+// ---- kernels --------------------------------------------------------------------
+constexpr int BLOCK = 256;               // 4 waves; each wave owns one 64-codeword tile at a time
+constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
+#ifndef TDEC_WIN
+#define TDEC_WIN 2
+#endif
+constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval (must divide N; every table N is a multiple of 4)
+
+// Plane layout of one 64-codeword tile: [2][N][64] float4
+//   X[k] = {A[k], B[k], W1[k], Y1[k]}            decoder 1, natural order
+//   Z[k] = {A[perm[k]], B[perm[k]], W2[k], Y2[k]} decoder 2 (:507-512); .xy filled per tile
+struct DecodeArgs {
+    int B, N, iters, n_tiles, n_waves;
+    float4 *planes;          // [n_tiles][2][N][64]
+    double2 *le;             // [n_waves][2][N][64]: Le1, Le2 as {A, B}
+    float4 *ck;              // [n_waves][N/WIN][4][64]
+    int32_t *bits;           // [B][2N]
+    double *lfinal;          // [B][2N] or null
+};
+
+// DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
+template <int ALGO>
+__global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int *__restrict__ perm,
+                                                       const int *__restrict__ inv) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (wave >= p.n_waves) return;
+    const int N = p.N;
+    const long NW = (long)N * WAVE;
+    double2 *Le1 = p.le + (long)wave * 2 * NW, *Le2 = Le1 + NW;
+    float4 *ck = p.ck + (long)wave * (N / WIN) * 4 * WAVE;
+    for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
+        float4 *X = p.planes + (long)tile * 2 * NW, *Z = X + NW;
+        // interleaved systematic LLRs for decoder 2 (:511-512)
+        for (int k = 0; k < N; ++k) {
+            const float4 x = X[(long)perm[k] * WAVE + lane];
+            float4 z = Z[(long)k * WAVE + lane];
+            z.x = x.x;
+            z.y = x.y;
+            Z[(long)k * WAVE + lane] = z;
+        }
+        for (int it = 0; it < p.iters; ++it) {
+            const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
+            siso<ALGO, WIN>(TileIn{X, it ? Le2 : nullptr, inv, lane}, TileOut{Le1, lane}, N, ck, lane, sf);
+            siso<ALGO, WIN>(TileIn{Z, Le1, perm, lane}, TileOut{Le2, lane}, N, ck, lane, sf);
+        }
+        // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
+        const long cw = (long)tile * WAVE + lane;
+        if (cw < p.B) {
+            int32_t *bo = p.bits + cw * 2 * N;
+            double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
+            for (int k = 0; k < N; ++k) {
+                const float4 x = X[(long)k * WAVE + lane];
+                const double2 la = Le2[(long)inv[k] * WAVE + lane];
+                const double2 le = Le1[(long)k * WAVE + lane];
+                const double fa = ((double)x.x + la.x) + le.x;
+                const double fb = ((double)x.y + la.y) + le.y;
+                *reinterpret_cast<int2 *>(bo + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
+                if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
+            }
+        }
+    }
+}
+
+// One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).
+struct SisoArgs {
+    int B, N, n_waves;
+    const float *LcA, *LcB, *LcW, *LcY;
+    const double *LaA, *LaB;
+    double sf;
+    double *LeA, *LeB;
+    float4 *ck;
+};
+
+template <int ALGO>
+__global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (wave >= p.n_waves) return;
+    const long cw = (long)wave * WAVE + lane;
+    const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
+    float4 *ck = p.ck + (long)wave * (p.N / WIN) * 4 * WAVE;
+    RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
+    siso<ALGO, WIN>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, lane, p.sf);
+}
+
+// De-puncture (:468-487): llr rows -> tile planes X (all four) and Z (.zw only).
+// src[c*N + k] = LLR index or -1 for the 8 components c = X.xyzw, Z.xyzw
+// (Z.xy are -1 here: the decode kernel gathers them through perm).
+__global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float *llr, long stride, const int *src,
+                                                     float4 *planes, long total) {
+    const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= total) return;                 // total = tiles * 2 * N * 64
+    const int lane = (int)(t & (WAVE - 1));
+    const long q = t >> 6;                  // (tile, half, k)
+    const long hk = q % (2L * N);
+    const long tile = q / (2L * N);
+    const long cw = tile * WAVE + lane;
+    const int half = (int)(hk / N), k = (int)(hk % N);
+    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (cw < B) {
+        const float *row = llr + cw * stride;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = src[(long)(half * 4 + c) * N + k];
+            if (j >= 0) v[c] = row[j];
+        }
+    }
+    planes[t] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// ---- soft demapper (compute_llr, test_sdr_with_coding.py:200-225) -----------------
+// numpy's complex |z| (SIMD loop of umath, FMA host): larger*sqrt(fma(r,r,1)).
+template <typename T> __device__ __forceinline__ T cabs_np(T re, T im) {
+    const T inf = (T)INFINITY;
+    re = fabs(re);
+    im = fabs(im);
+    const bool re_inf = re == inf, im_inf = im == inf;
+    im = re_inf ? inf : im;
+    re = im_inf ? inf : re;
+    const bool re_nn = re == re, im_nn = im == im;
+    im = re_nn ? im : (T)NAN;
+    re = im_nn ? re : (T)NAN;
+    const T larger = re > im ? re : im;
+    const T smaller = im < re ? im : re;
+    const bool div = !(larger == (T)0 || smaller == inf);
+    const T ratio = div ? smaller / larger : (T)0;
+    const T h = sqrt(fma(ratio, ratio, (T)1));
+    return h * larger;
+}
+
+struct DemapCfg {
+    int M, div_f32, sign;
+    double nv;                 // max(noise_var, 0.005) already applied (:202)
+};
+
+// All BPS LLRs of one symbol, reference sign (positive -> bit 1) unless
+// c.sign < 0.  Streams over the M points keeping a running min per bit and
+// label value, so no distance array is materialised.
+template <typename T, int BPS>
+__device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    T m0[BPS], m1[BPS];
+    bool n0[BPS], n1[BPS];
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) {
+        m0[b] = m1[b] = (T)INFINITY;
+        n0[b] = n1[b] = false;
+    }
+    for (int m = 0; m < c.M; ++m) {
+        const T a = cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
+        const T v = a * a;                     // np.abs(s - constellation) ** 2
+        const bool vn = v != v;
+#pragma unroll
+        for (int b = 0; b < BPS; ++b) {
+            if ((m >> (BPS - 1 - b)) & 1) {
+                n1[b] |= vn;
+                m1[b] = v < m1[b] ? v : m1[b];
+            } else {
+                n0[b] |= vn;
+                m0[b] = v < m0[b] ? v : m0[b];
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) {
+        const T lo = n0[b] ? (T)NAN : m0[b];   // np.min propagates NaN
+        const T hi = n1[b] ? (T)NAN : m1[b];
+        const T diff = lo - hi;
+        double v;
+        if (sizeof(T) == 4 && c.div_f32) v = (double)((float)diff / (float)c.nv);
+        else v = (double)diff / c.nv;
+        if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);   // np.clip(llr, -30, 30)
+        out[b] = c.sign < 0 ? -v : v;
+    }
+}
+
+template <typename T, typename S, int BPS>
+__global__ __launch_bounds__(BLOCK) void k_demap(const S *syms, long n_sym, const T *cons_g, DemapCfg c, double *llr) {
+    __shared__ T cons[512];
+    for (int i = threadIdx.x; i < 2 * c.M; i += BLOCK) cons[i] = cons_g[i];
+    __syncthreads();
+    const long s = (long)blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n_sym) return;
+    double v[BPS];
+    sym_llrs<T, BPS>((T)syms[2 * s], (T)syms[2 * s + 1], cons, c, v);
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) llr[s * BPS + b] = v[b];
+}
+
+// Fused demap -> f32 -> de-puncture planes (the bench path).  Thread =
+// (codeword, symbol) with the codeword fastest.  dst[j] = (half*N + k)*4 + c:
+// the float4 component of the tile planes that LLR index j < n_llr feeds.
+template <typename T, int BPS>
+__global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
+                                                       DemapCfg c, const int *dst, long n_llr, float *planes) {
+    __shared__ T cons[512];
+    for (int i = threadIdx.x; i < 2 * c.M; i += BLOCK) cons[i] = cons_g[i];
+    __syncthreads();
+    const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
+    const long n_tiles = (B + WAVE - 1) / WAVE;
+    if (t >= n_tiles * WAVE * S) return;
+    const int lane = (int)(t & (WAVE - 1));
+    const long q = t >> 6;
+    const long s = q % S, tile = q / S;
+    const long cw = tile * WAVE + lane;
+    if (cw >= B) return;
+    const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+    double v[BPS];
+    sym_llrs<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+    float *P = planes + tile * 2L * N * WAVE * 4 + lane * 4;
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) {
+        const long j = s * BPS + b;
+        if (j < n_llr) {
+            const long d = dst[j];
+            P[(d >> 2) * WAVE * 4 + (d & 3)] = (float)v[b];   // decode(): np.array(llr, float32)
+        }
+    }
+}
+
+// ---- encoder (workload generation; encode, :404-462) ------------------------------
+struct EncodeArgs {
+    int B, N, period;
+    long n_out;
+    unsigned char punct[16];
+    int circ[16];
+    const int *perm;
+    const uint8_t *bits;
+    uint8_t *coded;
+};
+
+__device__ __forceinline__ int next_rt(int s, int inp) {
+    const int dk = ((inp >> 1) & 1) ^ (inp & 1) ^ ((s >> 2) & 1) ^ ((s >> 3) & 1);
+    return (((s >> 2) & 1) << 3) | (((s >> 1) & 1) << 2) | ((s & 1) << 1) | dk;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_encode(EncodeArgs p) {
+    const long cw = (long)blockIdx.x * BLOCK + threadIdx.x;
+    if (cw >= p.B) return;
+    const uint8_t *u = p.bits + cw * 2 * p.N;
+    uint8_t *o = p.coded + cw * p.n_out;
+    int s1 = 0, s2 = 0;
+    for (int i = 0; i < p.N; ++i) {
+        const int j = p.perm[i];
+        s1 = next_rt(s1, (u[2 * i] << 1) | u[2 * i + 1]);
+        s2 = next_rt(s2, (u[2 * j] << 1) | u[2 * j + 1]);
+    }
+    s1 = p.circ[s1];
+    s2 = p.circ[s2];
+    long q = 0;
+    for (int i = 0; i < p.N; ++i) {
+        const int j = p.perm[i], ph = i % p.period;
+        const int i1 = (u[2 * i] << 1) | u[2 * i + 1], i2 = (u[2 * j] << 1) | u[2 * j + 1];
+        const int dk1 = ((i1 >> 1) & 1) ^ (i1 & 1) ^ ((s1 >> 2) & 1) ^ ((s1 >> 3) & 1);
+        const int dk2 = ((i2 >> 1) & 1) ^ (i2 & 1) ^ ((s2 >> 2) & 1) ^ ((s2 >> 3) & 1);
+        o[q++] = u[2 * i];
+        o[q++] = u[2 * i + 1];
+        if (p.punct[0 * 4 + ph]) o[q++] = dk1 ^ (s1 & 1) ^ ((s1 >> 1) & 1) ^ ((s1 >> 3) & 1);
+        if (p.punct[1 * 4 + ph]) o[q++] = dk1 ^ ((s1 >> 1) & 1) ^ ((s1 >> 2) & 1) ^ ((s1 >> 3) & 1);
+        if (p.punct[2 * 4 + ph]) o[q++] = dk2 ^ (s2 & 1) ^ ((s2 >> 1) & 1) ^ ((s2 >> 3) & 1);
+        if (p.punct[3 * 4 + ph]) o[q++] = dk2 ^ ((s2 >> 1) & 1) ^ ((s2 >> 2) & 1) ^ ((s2 >> 3) & 1);
+        s1 = next_rt(s1, i1);
+        s2 = next_rt(s2, i2);
+    }
+}
+
+}  // namespace tdec

@@ -1,0 +1,299 @@
+"""Drop-in replacement for the reference module ``dvb_rcs2_turbo``
+(poriya219/modulations, dvb_rcs2_turbo.py), decode side on MI355X.
+
+Same names, argument meaning, dtypes and error behaviour as the reference:
+
+* ``DVBRCS2_Turbo(N_couples, code_rate, iterations=8)``   -- :287-537
+  ``.decode(llr) -> int32[2N]``, ``.encode(bits) -> int32[n_coded]`` and the
+  attributes ``N, k_info, n_coded, iterations, punct, perm, inv_perm,
+  next_state, out_W, out_Y, prev_state, prev_input, G_matrix``.
+* ``bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y,
+  prev_st, prev_inp, N, scaling_factor) -> (Le_A, Le_B)``   -- :116-281
+* ``max_star``, ``mat_mul_gf2``, ``mat_pow_gf2``, ``solve_circular_state_gf2``,
+  ``INTERLEAVER_PARAMS``, ``PUNCTURE_PATTERNS``             -- :9-114
+* the north-star names ``bcjr_decode_circular`` (= bcjr_max_log_map) and
+  ``turbo_decode(llr, N_couples, code_rate, iterations=8)``.
+
+Additions: ``decode_batch`` (B codewords in one launch), ``decode_device``
+(torch tensors already on the GPU, stream-ordered), ``algo='log-map'``,
+``inv_perm=`` / ``interleaver=`` to pin the de-interleaver.
+
+Every decode / SISO runs in the HIP library (modulations_amd/lib/libtdec.so);
+there is no host fallback.  ``encode`` is host-side numpy (it is not on the hot
+path; the batched device encoder is ``encode_device``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as _n
+from . import tables as _t
+from .tables import (INTERLEAVER_PARAMS, PUNCTURE_PATTERNS, mat_mul_gf2, mat_pow_gf2, max_star,  # noqa: F401
+                     solve_circular_state_gf2)
+
+ALGOS = {"max-log": 0, "maxlog": 0, "max-log-map": 0, "log-map": 1, "logmap": 1}
+
+_TABLES = None
+
+
+def _std_tables():
+    global _TABLES
+    if _TABLES is None:
+        _TABLES = _t.trellis_tables()
+    return _TABLES
+
+
+class _Handle:
+    """Owns one tdec_t (device-side codec state)."""
+
+    def __init__(self, device, n, punct, iterations, algo, perm, inv_perm, tables):
+        pm = np.ascontiguousarray(_t.puncture_matrix(punct))
+        self._keep = (pm, np.ascontiguousarray(perm, np.int32), np.ascontiguousarray(inv_perm, np.int32),
+                      np.ascontiguousarray(tables, np.int32))
+        h = C.c_void_p()
+        _n.check(_n.lib().tdec_create(device, n, punct["period"], _n.ptr(pm), iterations, algo,
+                                      _n.ptr(self._keep[1]), _n.ptr(self._keep[2]), _n.ptr(self._keep[3]),
+                                      C.byref(h)))
+        self.h = h
+        self.device = device
+        self.llr_len = _n.lib().tdec_llr_len(h)
+        self.enc_len = _n.lib().tdec_encoded_len(h)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value and _n._lib is not None:
+            _n._lib.tdec_destroy(h)
+            self.h = None
+
+
+def _default_device():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.cuda.current_device()
+    except Exception:  # pragma: no cover - torch is optional for the host API
+        pass
+    return 0
+
+
+class DVBRCS2_Turbo:
+    """DVB-RCS2 duo-binary turbo codec (reference :287-537), decode on MI355X.
+
+    Extra keyword arguments (all optional, defaults reproduce the reference):
+      algo       'max-log' (reference) or 'log-map' (build-defined max* with correction)
+      inv_perm   'stable' (default: np.argsort(perm, kind='stable'), host independent),
+                 'numpy' (the reference's np.argsort(perm) evaluated on this host),
+                 or an explicit int array
+      interleaver 'reference' (default; the reference's non-bijective perm) or
+                 'valid-perm' (a true permutation: never used for parity)
+      device     HIP device ordinal
+    """
+
+    def __init__(self, N_couples, code_rate, iterations=8, *, algo="max-log", inv_perm="stable",
+                 interleaver="reference", device=None):
+        self.N = N_couples
+        self.k_info = N_couples * 2
+        self.iterations = iterations
+        self.punct = PUNCTURE_PATTERNS[code_rate]          # KeyError for an unknown rate, as :292
+        if self.N not in INTERLEAVER_PARAMS:
+            raise ValueError(f"Block size {self.N} not in standard tables.")
+        self.code_rate = code_rate
+        self.algo = ALGOS[algo] if isinstance(algo, str) else int(algo)
+        if interleaver == "reference":
+            self.perm = _t.interleaver(self.N)
+        elif interleaver == "valid-perm":
+            self.perm = _t.valid_interleaver(self.N)
+        else:
+            raise ValueError(f"unknown interleaver {interleaver!r}")
+        if isinstance(inv_perm, str):
+            self.inv_perm = (_t.inverse_interleaver(self.perm, inv_perm) if interleaver == "reference"
+                             else np.argsort(self.perm).astype(np.int32))
+        else:
+            self.inv_perm = np.ascontiguousarray(inv_perm, np.int32)
+        (self.next_state, self.out_W, self.out_Y, self.prev_state, self.prev_input,
+         self.G_matrix) = _std_tables()
+        self.n_coded = _t.coded_size(self.N, self.punct)
+        self.device = _default_device() if device is None else device
+        self._h = None
+        self._circ = None
+
+    # -- device handle (created lazily so a codec can be built without a GPU) --
+    @property
+    def handle(self):
+        if self._h is None:
+            tabs = _t.packed_tables(self.next_state, self.out_W, self.out_Y, self.prev_state, self.prev_input)
+            self._h = _Handle(self.device, self.N, self.punct, self.iterations, self.algo, self.perm,
+                              self.inv_perm, tabs)
+        return self._h
+
+    # -- encode (host; :404-462) -----------------------------------------------------
+    def _encode_component(self, A, B):
+        state = 0
+        for i in range(self.N):
+            state = self.next_state[state, (A[i] << 1) | B[i]]
+        if self._circ is None:
+            self._circ = _t.circular_state_table(self.N, self.G_matrix)
+        state = int(self._circ[state])
+        W = np.zeros(self.N, dtype=np.int32)
+        Y = np.zeros(self.N, dtype=np.int32)
+        for i in range(self.N):
+            inp = (A[i] << 1) | B[i]
+            W[i] = self.out_W[state, inp]
+            Y[i] = self.out_Y[state, inp]
+            state = self.next_state[state, inp]
+        return W, Y
+
+    def encode(self, bits):
+        """Encode bits into a DVB-RCS2 turbo codeword (reference :431-462)."""
+        bits = np.array(bits, dtype=np.int32)
+        A = bits[0::2]
+        B = bits[1::2]
+        W1, Y1 = self._encode_component(A, B)
+        W2, Y2 = self._encode_component(A[self.perm], B[self.perm])
+        coded = []
+        period = self.punct['period']
+        for i in range(self.N):
+            p = i % period
+            coded.append(A[i])
+            coded.append(B[i])
+            if self.punct['W1'][p]: coded.append(W1[i])
+            if self.punct['Y1'][p]: coded.append(Y1[i])
+            if self.punct['W2'][p]: coded.append(W2[i])
+            if self.punct['Y2'][p]: coded.append(Y2[i])
+        return np.array(coded, dtype=np.int32)
+
+    # -- decode (:464-537) -----------------------------------------------------------
+    def decode(self, llr):
+        """Decode one codeword's LLRs (LLR = log P(0)/P(1)) into int32[2N] info bits."""
+        llr = np.array(llr, dtype=np.float32)
+        if llr.ndim != 1:
+            raise ValueError("decode() takes one codeword; use decode_batch for [B, n] input")
+        return self.decode_batch(llr[None, :])[0]
+
+    def decode_batch(self, llr, return_lfinal=False):
+        """Decode B codewords: llr [B, >= n_llr] -> int32 [B, 2N]
+        (and L_final f64 [B, 2N] = Lc + La + Le1, :529-530, when asked)."""
+        llr = np.ascontiguousarray(np.asarray(llr, dtype=np.float32))
+        if llr.ndim != 2:
+            raise ValueError("decode_batch takes a [B, n] array")
+        h = self.handle
+        if llr.shape[1] < h.llr_len:
+            raise IndexError(f"index {llr.shape[1]} is out of bounds for axis 0 with size {llr.shape[1]}")
+        B = llr.shape[0]
+        bits = np.zeros((B, self.k_info), np.int32)
+        lf = np.zeros((B, self.k_info)) if return_lfinal else None
+        if B:
+            _n.check(_n.lib().tdec_decode_batch(h.h, B, _n.ptr(llr), llr.shape[1], _n.ptr(bits), _n.ptr(lf)))
+        return (bits, lf) if return_lfinal else bits
+
+    # -- device-resident API (torch tensors on this codec's GPU) -------------------------
+    def reserve(self, max_batch):
+        _n.check(_n.lib().tdec_reserve(self.handle.h, int(max_batch)))
+
+    def planes_bytes(self, B):
+        return _n.lib().tdec_planes_bytes(self.handle.h, int(B))
+
+    def decode_device(self, llr, bits=None, lfinal=None, stream=None):
+        """llr: float32 [B, n] device tensor -> int32 [B, 2N] device tensor."""
+        import torch
+        B = llr.shape[0]
+        self.reserve(B)
+        if bits is None:
+            bits = torch.empty((B, self.k_info), dtype=torch.int32, device=llr.device)
+        _n.check(_n.lib().tdec_decode_batch_dev(self.handle.h, B, _n.ptr(llr), llr.stride(0), _n.ptr(bits),
+                                                _n.ptr(lfinal), _n.stream_ptr(stream)))
+        return bits
+
+    def decode_planes_device(self, planes, B, bits, lfinal=None, stream=None):
+        _n.check(_n.lib().tdec_decode_planes_dev(self.handle.h, B, _n.ptr(planes), _n.ptr(bits), _n.ptr(lfinal),
+                                                 _n.stream_ptr(stream)))
+        return bits
+
+    def depuncture_device(self, llr, planes, stream=None):
+        _n.check(_n.lib().tdec_depuncture_dev(self.handle.h, llr.shape[0], _n.ptr(llr), llr.stride(0),
+                                              _n.ptr(planes), _n.stream_ptr(stream)))
+        return planes
+
+    def demap_planes_device(self, syms, constellation, bps, noise_var, planes, div_f32=False, stream=None):
+        """Fused soft demap (decoder sign) + de-puncture of complex64 symbols [B, S]."""
+        cons = np.ascontiguousarray(np.asarray(constellation))
+        f64 = cons.dtype == np.complex128
+        cons = cons.astype(np.complex128 if f64 else np.complex64)
+        B, S = syms.shape[0], syms.shape[1]
+        _n.check(_n.lib().tdec_demap_planes_dev(self.handle.h, B, _n.ptr(syms), S, _n.ptr(cons), int(f64),
+                                                len(cons), bps, float(noise_var), int(div_f32), _n.ptr(planes),
+                                                _n.stream_ptr(stream)))
+        return planes
+
+    def encode_device(self, bits_u8, coded_u8=None, stream=None):
+        """Batched device encoder: uint8 [B, 2N] -> uint8 [B, n_out] (same bits as encode())."""
+        import torch
+        B = bits_u8.shape[0]
+        if coded_u8 is None:
+            coded_u8 = torch.empty((B, self.handle.enc_len), dtype=torch.uint8, device=bits_u8.device)
+        _n.check(_n.lib().tdec_encode_dev(self.handle.h, B, _n.ptr(bits_u8), _n.ptr(coded_u8),
+                                          _n.stream_ptr(stream)))
+        return coded_u8
+
+
+# ---- module-level functions of the reference ------------------------------------------
+
+_SISO_CACHE = {}
+
+
+def bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,
+                     scaling_factor):
+    """Max-Log-MAP SISO (reference :116-281), one codeword, on the GPU.
+
+    Same arguments and outputs: f32 channel LLRs, f64 a-priori, the five int32
+    [16,4] trellis tables, N couples and the extrinsic scaling factor; returns
+    freshly allocated (Le_A, Le_B) f64 arrays.  Inputs are not mutated.
+    """
+    LeA, LeB = bcjr_max_log_map_batch(np.asarray(Lc_A)[None], np.asarray(Lc_B)[None], np.asarray(Lc_W)[None],
+                                      np.asarray(Lc_Y)[None], np.asarray(La_A)[None], np.asarray(La_B)[None],
+                                      next_st, out_W, out_Y, prev_st, prev_inp, N, scaling_factor)
+    return LeA[0], LeB[0]
+
+
+bcjr_decode_circular = bcjr_max_log_map   # historic name of the same SISO
+
+
+def bcjr_max_log_map_batch(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,
+                           scaling_factor, algo="max-log", device=None):
+    """bcjr_max_log_map over B codewords at once: [B, N] arrays in, (Le_A, Le_B) [B, N] out."""
+    N = int(N)
+    f32 = lambda x: np.ascontiguousarray(np.asarray(x, np.float32)[:, :N])
+    f64 = lambda x: np.ascontiguousarray(np.asarray(x, np.float64)[:, :N])
+    A, Bv, W, Y, la, lb = f32(Lc_A), f32(Lc_B), f32(Lc_W), f32(Lc_Y), f64(La_A), f64(La_B)
+    for x in (A, Bv, W, Y, la, lb):
+        if x.shape[1] < N:
+            raise IndexError(f"index {x.shape[1]} is out of bounds for axis 0 with size {x.shape[1]}")
+    tabs = _t.packed_tables(next_st, out_W, out_Y, prev_st, prev_inp)
+    dev = _default_device() if device is None else device
+    key = (N, tabs.tobytes(), ALGOS[algo] if isinstance(algo, str) else int(algo), dev)
+    h = _SISO_CACHE.get(key)
+    if h is None:
+        ident = np.arange(N, dtype=np.int32)
+        h = _Handle(dev, N, PUNCTURE_PATTERNS['1/3'], 1, key[2], ident, ident, tabs)
+        _SISO_CACHE[key] = h
+    B = A.shape[0]
+    LeA = np.zeros((B, N))
+    LeB = np.zeros((B, N))
+    _n.check(_n.lib().tdec_siso_batch(h.h, B, _n.ptr(A), _n.ptr(Bv), _n.ptr(W), _n.ptr(Y), _n.ptr(la), _n.ptr(lb),
+                                      float(scaling_factor), _n.ptr(LeA), _n.ptr(LeB)))
+    return LeA, LeB
+
+
+_CODEC_CACHE = {}
+
+
+def turbo_decode(llr, N_couples, code_rate, iterations=8, **kw):
+    """Historic module-level decode: DVBRCS2_Turbo(...).decode(llr)."""
+    key = (N_couples, code_rate, iterations, tuple(sorted(kw.items())))
+    c = _CODEC_CACHE.get(key)
+    if c is None:
+        c = _CODEC_CACHE[key] = DVBRCS2_Turbo(N_couples, code_rate, iterations, **kw)
+    llr = np.asarray(llr)
+    return c.decode_batch(llr) if llr.ndim == 2 else c.decode(llr)

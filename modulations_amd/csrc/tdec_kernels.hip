@@ -72,12 +72,44 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
 }
 
 // ---- max / max* ---------------------------------------------------------------
-// log-MAP (build-defined): Jacobian log with the historic 37 cut-off.
+// log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) with the
+// historic 37 cut-off.  The correction is defined as this exact sequence of f32
+// IEEE operations (no FMA: -ffp-contract=off; correctly rounded division), the
+// same sequence the oracle restates, so log-MAP is bit-exact too.
+__device__ __forceinline__ float jac_corr(float d) {   // log1p(exp(-d)), 0 <= d <= 37
+    const float x0 = d * 1.44269504088896341f;
+    const int n = (int)x0;
+    const float fn = (float)n;
+    const float r = (d - fn * 0.693145751953125f) - fn * 1.42860682030941723212e-6f;
+    const float x = -r;
+    float p = 1.0f / 40320.0f;
+    p = p * x + 1.0f / 5040.0f;
+    p = p * x + 1.0f / 720.0f;
+    p = p * x + 1.0f / 120.0f;
+    p = p * x + 1.0f / 24.0f;
+    p = p * x + 1.0f / 6.0f;
+    p = p * x + 0.5f;
+    p = p * x + 1.0f;
+    p = p * x + 1.0f;
+    const float e = ldexpf(p, -n);
+    const float u = e / (2.0f + e);
+    const float u2 = u * u;
+    float q = 1.0f / 15.0f;
+    q = q * u2 + 1.0f / 13.0f;
+    q = q * u2 + 1.0f / 11.0f;
+    q = q * u2 + 1.0f / 9.0f;
+    q = q * u2 + 1.0f / 7.0f;
+    q = q * u2 + 1.0f / 5.0f;
+    q = q * u2 + 1.0f / 3.0f;
+    q = q * u2 + 1.0f;
+    return (2.0f * u) * q;
+}
+
 __device__ __forceinline__ float jac(float a, float b) {
     const float m = a > b ? a : b;
     const float d = fabsf(a - b);
-    const float c = log1pf(expf(-d));
-    return (d <= 37.0f) ? m + c : m;     // NaN d and d > 37 keep m
+    const float c = jac_corr(d <= 37.0f ? d : 0.0f);   // branch-free; operand kept in range
+    return (d <= 37.0f) ? m + c : m;                     // NaN d and d > 37 keep m
 }
 
 template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {

@@ -46,6 +46,8 @@ def lib():
         L.orc_encode.restype = C.c_long
         L.orc_demap_c64.argtypes = [_f32p, C.c_long, _f32p, C.c_int, C.c_int, C.c_double, C.c_int, _f64p]
         L.orc_demap_c128.argtypes = [_f64p, C.c_long, _f64p, C.c_int, C.c_int, C.c_double, _f64p]
+        L.orc_jac.argtypes = [C.c_float, C.c_float]
+        L.orc_jac.restype = C.c_float
         _lib = L
     return _lib
 

@@ -92,16 +92,52 @@ void orc_interleaver(int N, const int32_t *params, int32_t *perm, int32_t *inv_s
 
 static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
 
-/* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm with the
- * cut-off of the historic _jacobian_log-22; evaluated in f32. */
+/* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm
+ * max(a,b) + log1p(exp(-|a-b|)), with the cut-off (|a-b| > 37 -> max) of the
+ * historic _jacobian_log-22.  The correction is DEFINED as the fixed sequence of
+ * f32 IEEE operations below (Cody-Waite reduction, degree-8 Taylor exp, atanh
+ * series for log1p; |error| < 1e-7 against the real function), so that the
+ * HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr) restates it
+ * bit for bit instead of depending on two different libms. */
+static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
+{
+    const float x0 = d * 1.44269504088896341f;
+    const int n = (int)x0;
+    const float fn = (float)n;
+    const float r = (d - fn * 0.693145751953125f) - fn * 1.42860682030941723212e-6f;
+    const float x = -r;
+    float p = 1.0f / 40320.0f;
+    p = p * x + 1.0f / 5040.0f;
+    p = p * x + 1.0f / 720.0f;
+    p = p * x + 1.0f / 120.0f;
+    p = p * x + 1.0f / 24.0f;
+    p = p * x + 1.0f / 6.0f;
+    p = p * x + 0.5f;
+    p = p * x + 1.0f;
+    p = p * x + 1.0f;
+    const float e = ldexpf(p, -n);
+    const float u = e / (2.0f + e);
+    const float u2 = u * u;
+    float q = 1.0f / 15.0f;
+    q = q * u2 + 1.0f / 13.0f;
+    q = q * u2 + 1.0f / 11.0f;
+    q = q * u2 + 1.0f / 9.0f;
+    q = q * u2 + 1.0f / 7.0f;
+    q = q * u2 + 1.0f / 5.0f;
+    q = q * u2 + 1.0f / 3.0f;
+    q = q * u2 + 1.0f;
+    return (2.0f * u) * q;
+}
+
 static inline float jac(float a, float b)
 {
     float m = a > b ? a : b;
     float d = fabsf(a - b);
-    if (d != d) return m;              /* NaN: keep the max-log behaviour */
-    if (d > 37.0f) return m;
-    return m + log1pf(expf(-d));
+    if (!(d <= 37.0f)) return m;       /* NaN d or d > 37: plain max */
+    return m + jac_corr(d);
 }
+
+float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy test */
 
 static inline float star(int algo, float a, float b)
 {

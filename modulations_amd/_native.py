@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libtdec.so")
+# A/B experiments only: TDEC_LIB_VARIANT=w4 loads lib/libtdec_w4.so (built by build.py --variant)
+if os.environ.get("TDEC_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, "lib", f"libtdec_{os.environ['TDEC_LIB_VARIANT']}.so")
 
 TDEC_OK, TDEC_EINVAL, TDEC_ESHORT, TDEC_ENOMEM, TDEC_EHIP, TDEC_EUNSUPPORTED, TDEC_EITER, TDEC_ECAPACITY = \
     0, -1, -2, -3, -4, -5, -6, -7

@@ -38,5 +38,20 @@ def build(force=False, extra=()):
     return OUT
 
 
+def build_variant(name, defines):
+    """Side-by-side variant for A/B timing (lib/libtdec_<name>.so)."""
+    out = os.path.join(HERE, "lib", f"libtdec_{name}.so")
+    cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"), "-o", out, SRC]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed building {out}")
+    return out
+
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:]))
+    else:
+        print(build(force="--force" in sys.argv))

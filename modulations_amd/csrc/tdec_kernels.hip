@@ -240,10 +240,12 @@ struct RowOut {
 
 // bcjr_max_log_map (:116-281) for the calling lane's codeword.
 // ck: checkpoint ring of this wave, [(N/W)][4][64] float4 (uniform base).
-// Inputs are software-pipelined one group of W steps ahead.
+// Inputs are software-pipelined one group of W steps ahead: a group's raw
+// inputs are turned into branch metrics first, then the next group's loads are
+// issued into the same registers, then the group's recursion steps run.
 template <int ALGO, int W, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, double sf) {
-    Raw cur[W], nxt[W];
+    Raw raw[W];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
@@ -251,11 +253,17 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
     // (:182-183); pass 2 checkpoints alpha every W steps.
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-        for (int j = 0; j < W; ++j) cur[j] = in.load(j);
+        for (int j = 0; j < W; ++j) raw[j] = in.load(j);
         for (int k0 = 0; k0 < N; k0 += W) {
+            float g[W][8];
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                double iA, iB;
+                gamma_of(raw[j], g[j], iA, iB);
+            }
             if (k0 + W < N) {
 #pragma unroll
-                for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 + W + j);
+                for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
             }
             if (pass) {
                 float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
@@ -263,14 +271,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
                 for (int q = 0; q < 4; ++q) c[q * WAVE] = make_float4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
             }
 #pragma unroll
-            for (int j = 0; j < W; ++j) {
-                float g[8];
-                double iA, iB;
-                gamma_of(cur[j], g, iA, iB);
-                alpha_step<ALGO>(a, g);
-            }
-#pragma unroll
-            for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+            for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
         }
     }
     // backward pass 1 (:203-213)
@@ -278,59 +279,63 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < W; ++j) cur[j] = in.load(N - W + j);
+    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
     for (int k0 = N - W; k0 >= 0; k0 -= W) {
+        float g[W][8];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            double iA, iB;
+            gamma_of(raw[j], g[j], iA, iB);
+        }
         if (k0 > 0) {
 #pragma unroll
-            for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 - W + j);
+            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
         }
 #pragma unroll
-        for (int j = W - 1; j >= 0; --j) {
-            float g[8];
-            double iA, iB;
-            gamma_of(cur[j], g, iA, iB);
-            beta_step<ALGO>(b, g);
-        }
-#pragma unroll
-        for (int j = 0; j < W; ++j) cur[j] = nxt[j];
+        for (int j = W - 1; j >= 0; --j) beta_step<ALGO>(b, g[j]);
     }
     // beta[N] = beta[0] (:216-217); backward pass 2 fused with the extrinsic
-    // (:220-281), alpha recomputed per window from its checkpoint.
+    // (:220-281).  alpha[k] of pass 2 is recomputed from the window's
+    // checkpoint (the same f32 operations, so bit-exact): holding all W alpha
+    // vectors of a window costs 16*W VGPRs, recomputing costs W(W-1)/2 extra
+    // steps per window of VALU, which this HBM-bound kernel has to spare.
 #pragma unroll
-    for (int j = 0; j < W; ++j) cur[j] = in.load(N - W + j);
+    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
     for (int k0 = N - W; k0 >= 0; k0 -= W) {
-        if (k0 > 0) {
-#pragma unroll
-            for (int j = 0; j < W; ++j) nxt[j] = in.load(k0 - W + j);
-        }
-        float aw[W][NS], gw[W][8];
+        float gw[W][8];
         double iAw[W], iBw[W];
 #pragma unroll
-        for (int j = 0; j < W; ++j) gamma_of(cur[j], gw[j], iAw[j], iBw[j]);
+        for (int j = 0; j < W; ++j) gamma_of(raw[j], gw[j], iAw[j], iBw[j]);
+        float a0[NS];
         const float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float4 v = c[q * WAVE];
-            aw[0][4 * q] = v.x;
-            aw[0][4 * q + 1] = v.y;
-            aw[0][4 * q + 2] = v.z;
-            aw[0][4 * q + 3] = v.w;
+            a0[4 * q] = v.x;
+            a0[4 * q + 1] = v.y;
+            a0[4 * q + 2] = v.z;
+            a0[4 * q + 3] = v.w;
         }
+        if (k0 > 0) {
 #pragma unroll
-        for (int j = 1; j < W; ++j) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s) aw[j][s] = aw[j - 1][s];
-            alpha_step<ALGO>(aw[j], gw[j - 1]);
+            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
         }
 #pragma unroll
         for (int j = W - 1; j >= 0; --j) {
+            __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
+            float aj[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                aj[s] = a0[s];
+                asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
+            }
+#pragma unroll
+            for (int i = 0; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
             double leA, leB;
-            extrinsic<ALGO>(aw[j], gw[j], b, iAw[j], iBw[j], sf, leA, leB);
+            extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
             out.store(k0 + j, leA, leB);
             beta_step<ALGO>(b, gw[j]);
         }
-#pragma unroll
-        for (int j = 0; j < W; ++j) cur[j] = nxt[j];
     }
 }
 
@@ -338,7 +343,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
 constexpr int BLOCK = 256;               // 4 waves; each wave owns one 64-codeword tile at a time
 constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 #ifndef TDEC_WIN
-#define TDEC_WIN 2
+#define TDEC_WIN 4
 #endif
 constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval (must divide N; every table N is a multiple of 4)
 

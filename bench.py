@@ -30,6 +30,8 @@ sys.path.insert(0, ROOT)
 
 from modulations_amd import demap as D  # noqa: E402
 from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402
+from modulations_amd import sharding as Sh  # noqa: E402
+from modulations_amd.workload import DevicePipeline, make_symbols  # noqa: E402
 
 VALU_PEAK = 256 * 4 * 32 * 2.4e9     # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
 HBM_PEAK = 8.0e12                    # B/s (spec)
@@ -37,30 +39,6 @@ HBM_PEAK = 8.0e12                    # B/s (spec)
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
-
-
-def make_workload(codec, B, bps, cons, ebn0_db, rate, seed, device):
-    """Synthetic symbols [B, S] complex64 on the device + the info bits."""
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    info = torch.randint(0, 2, (B, codec.k_info), generator=g, device=device, dtype=torch.uint8)
-    coded = codec.encode_device(info)                       # uint8 [B, n_coded]
-    n = coded.shape[1]
-    S = -(-n // bps)
-    if S * bps > n:                                         # zero-pad the last symbol as the mappers do
-        coded = torch.nn.functional.pad(coded, (0, S * bps - n))
-    w = (1 << torch.arange(bps - 1, -1, -1, device=device, dtype=torch.int32))
-    labels = (coded.view(B, S, bps).to(torch.int32) * w).sum(-1)
-    table = torch.from_numpy(np.ascontiguousarray(cons.astype(np.complex64))).to(device)
-    x = table[labels]                                       # [B, S] complex64
-    del coded, labels
-    es = float(np.mean(np.abs(cons) ** 2))
-    n0 = es / (rate * bps * 10 ** (ebn0_db / 10.0))
-    sigma = float(np.sqrt(n0 / 2))
-    noise = torch.randn((B, S, 2), generator=g, device=device, dtype=torch.float32) * sigma
-    y = x + torch.view_as_complex(noise)
-    del noise, x
-    return info, y.contiguous(), S, n0
 
 
 def cpu_baseline(codec, syms_host, cons, bps, nv, div32, seconds):
@@ -118,30 +96,24 @@ def main():
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
 
-    R = {"1/3": 1 / 3, "1/2": 1 / 2, "2/3": 2 / 3, "3/4": 3 / 4}[args.rate]
     codec = M.DVBRCS2_Turbo(args.n, args.rate, 8, algo=args.algo, device=device.index)
     bps = D.MODULATIONS[args.mod]["bps"]
     cons = D.constellation(args.mod)
     B = args.batch
     t0 = time.time()
-    info, syms, S, n0 = make_workload(codec, B, bps, cons, args.ebn0, R, 1_000_003 * rank + 12345, device)
+    info, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, Sh.shard_seed(12345, rank), device)
+    S = syms.shape[1]
     nv = np.float64(n0)
     f64, div32, nve = D.demap_mode(np.complex64, cons.dtype, nv)
-    codec.reserve(B)
-    planes = torch.empty(codec.planes_bytes(B) // 4, dtype=torch.float32, device=device)
-    bits = torch.empty((B, codec.k_info), dtype=torch.int32, device=device)
+    pipe = DevicePipeline(codec, args.mod, B, device)
+    bits = pipe.bits
     torch.cuda.synchronize()
     log(f"[rank {rank}] workload ready: {B} codewords x {S} symbols in {time.time() - t0:.1f}s")
 
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
-        codec.demap_planes_device(syms, cons, bps, nve, planes, div_f32=div32, stream=stream)
-        if ev is not None:
-            ev[0].record(stream)
-        codec.decode_planes_device(planes, B, bits, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
+        pipe.run(syms, nv, stream=stream, events=ev)
 
     for i in range(args.warmup):
         step()
@@ -166,9 +138,8 @@ def main():
     errs = (bits.to(torch.uint8) != info).sum(dim=1)
     cnt = torch.tensor([int(errs.sum()), int((errs > 0).sum()), B], dtype=torch.int64, device=device)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if dist:
-        tdist.all_reduce(cnt)
-        tdist.all_reduce(tmax, op=tdist.ReduceOp.MAX)
+    Sh.reduce_counters(cnt, tdist if dist else None)
+    Sh.reduce_max(tmax, tdist if dist else None)
     elapsed = float(tmax)
     total_cw = B * world * args.steps
     value = total_cw / elapsed
@@ -178,6 +149,14 @@ def main():
         alg_bytes = B * (4 * n_llr + 4 * codec.k_info)        # f32 LLRs in + int32 bits out per codeword
         achieved = alg_bytes / (dec_ms * 1e-3)
         ops = 2 * codec.iterations * codec.N * 768            # SURVEY §8(d) lane-op count per codeword
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        wl = (f"{args.mod} soft-LLR demap + DVB-RCS2 turbo N={args.n} couples ({2 * args.n} info bits) "
+              f"r={args.rate}, 8 it {args.algo}-MAP")
+        if os.path.exists(tf):
+            tr = json.load(open(tf)).get("k_turbo_decode", {})
+            if tr.get("workload") == wl:
+                traffic = tr["hbm_bytes_per_codeword"] * B      # measured HBM bytes per launch (rocprof PMC)
         valu_achieved = B * ops / (dec_ms * 1e-3)
         out = {
             "metric": "codewords/sec + info-bits/sec, N=1504 r=1/3 8-iter max-log-MAP @1/2/4/8 GPU",
@@ -199,9 +178,13 @@ def main():
                        "parallelism": f"codeword shards x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_turbo_decode", "achieved": achieved / 1e9,
                          "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": None,
-                         "note": "algorithmic bytes = 4*n_coded + 4*2N per codeword; the path is VALU-bound, "
-                                 "see valu"},
+                         "traffic": traffic,
+                         "traffic_GBps": (traffic / (dec_ms * 1e-3) / 1e9) if traffic else None,
+                         "note": "achieved = algorithmic bytes (4*n_coded f32 LLRs in + 4*2N int32 bits out per "
+                                 "codeword) / k_turbo_decode launch time; traffic = rocprof-measured HBM bytes per "
+                                 "launch (profiles/traffic.json): the per-lane decoder streams its alpha "
+                                 "checkpoints, a-priori and branch inputs through HBM on every pass, and that "
+                                 "stream (traffic_GBps) is what bounds it"},
             "valu": {"achieved": valu_achieved / 1e12, "peak": VALU_PEAK / 1e12, "unit": "T lane-op/s",
                      "frac": valu_achieved / VALU_PEAK, "ops_per_codeword": ops},
             "decode_kernel_ms": dec_ms,

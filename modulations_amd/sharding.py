@@ -1,0 +1,50 @@
+"""Codeword sharding across GPUs.
+
+Codewords are independent, so a job of T codewords splits into contiguous
+ranges, one per rank (one process per GPU, torch.distributed over RCCL on
+the box, gloo in the CPU tests).  Each rank generates its own inputs from a
+counter-based seed, decodes them with no data-path collective, and only the
+three integer error counters (bit errors, frame errors, codewords) are summed
+at the end -- a few bytes of all-reduce.
+"""
+from __future__ import annotations
+
+SEED_STRIDE = 1_000_003
+
+
+def shard_range(total, world, rank):
+    """Contiguous [start, start+count) of `total` codewords owned by `rank`;
+    the first total % world ranks get one extra."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    base, extra = divmod(int(total), world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def shard_seed(base_seed, rank, point=0):
+    """Reproducible per-(shard, sweep point) seed: base + 1_000_003*rank + 7919*point."""
+    return int(base_seed) + SEED_STRIDE * int(rank) + 7919 * int(point)
+
+
+def batches(count, batch):
+    """Split a shard of `count` codewords into launches of at most `batch`."""
+    out, done = [], 0
+    while done < count:
+        n = min(batch, count - done)
+        out.append((done, n))
+        done += n
+    return out
+
+
+def reduce_counters(counters, dist=None):
+    """Sum int64 counters over all ranks (in place) when a process group is up."""
+    if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
+    return counters
+
+
+def reduce_max(value_tensor, dist=None):
+    if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(value_tensor, op=dist.ReduceOp.MAX)
+    return value_tensor

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 run directory (kernel trace + PMC passes) of bench.py
+into profiles/<round>_summary.{json,md}.
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE come from separate --pmc passes, are in KiB, and on gfx950 FETCH_SIZE
+reads exactly half the bytes of a wide coalesced streaming read, so
+hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+
+usage: tools/prof_summary.py gpurun_out/r01 profiles/r01 [batch]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def short(name):
+    for k in ("k_turbo_decode", "k_demap_planes", "k_depuncture", "k_encode", "k_siso_batch", "k_demap"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def pmc(path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(src, dst, batch=1 << 20):
+    batch = int(batch)
+    out = {"source": src, "batch_codewords": batch, "kernels": {}}
+    stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
+    for r in stats:
+        k = short(r["Name"])
+        if k.startswith("k_"):
+            out["kernels"][k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                                 "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
+                                 "share_pct": float(r["Percentage"])}
+    counters = {}
+    for sub in ("fetch/f", "write/w", "sq/s", "tcc/t"):
+        p = os.path.join(src, sub + "_counter_collection.csv")
+        if os.path.exists(p):
+            counters.update(pmc(p))
+    for k, d in out["kernels"].items():
+        c = {cn: v for (kk, cn), v in counters.items() if kk == k}
+        d["counters"] = c
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            rd = 2 * c["FETCH_SIZE"] * 1024
+            wr = c["WRITE_SIZE"] * 1024
+            d["hbm_read_bytes"] = rd
+            d["hbm_write_bytes"] = wr
+            d["hbm_bytes_per_launch"] = rd + wr
+            d["hbm_GBps"] = (rd + wr) / (d["avg_ms"] * 1e-3) / 1e9
+            d["hbm_bytes_per_codeword"] = (rd + wr) / batch
+        if "TCC_HIT_sum" in c:
+            d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        if "SQ_WAVE_CYCLES" in c:
+            d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            d["valu_insts_per_codeword"] = c.get("SQ_INSTS_VALU", 0) * 64 / batch
+            # VALU issue-busy share: wave-instructions x 2 cycles (SIMD-32) / (1024 SIMDs x cycles)
+            if "GRBM_GUI_ACTIVE" in c:
+                pass
+            d["valu_busy_est"] = c.get("SQ_INSTS_VALU", 0) * 2 / (1024 * 2.4e9 * d["avg_ms"] * 1e-3)
+    json.dump(out, open(dst + "_summary.json", "w"), indent=1)
+    with open(dst + "_summary.md", "w") as f:
+        f.write(f"# rocprofv3 summary ({src}), batch = {batch} codewords\n\n")
+        f.write("| kernel | calls | avg ms | HBM GB/launch | HBM GB/s | B/codeword | L2 hit | VALU busy (est) | wait_any |\n")
+        f.write("|---|---|---|---|---|---|---|---|---|\n")
+        for k, d in out["kernels"].items():
+            f.write(f"| {k} | {d['calls']} | {d['avg_ms']:.2f} | {d.get('hbm_bytes_per_launch', 0) / 1e9:.1f} | "
+                    f"{d.get('hbm_GBps', 0):.0f} | {d.get('hbm_bytes_per_codeword', 0):.0f} | "
+                    f"{d.get('l2_hit_rate', 0):.2f} | {d.get('valu_busy_est', 0):.2f} | {d.get('wait_any_frac', 0):.2f} |\n")
+    print(open(dst + "_summary.md").read())
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

@@ -82,6 +82,9 @@ def main():
     ap.add_argument("--algo", default="max-log")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
+                    "several ranks on one GPU together with --all-on-device0")
+    ap.add_argument("--all-on-device0", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,8 +93,12 @@ def main():
     dist = world > 1
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev_idx = 0 if args.all_on_device0 else local
+        torch.cuda.set_device(dev_idx)
+        if args.dist_backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            tdist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
@@ -136,8 +143,9 @@ def main():
 
     # error counters (not timed): info-bit errors, frame errors, codewords
     errs = (bits.to(torch.uint8) != info).sum(dim=1)
-    cnt = torch.tensor([int(errs.sum()), int((errs > 0).sum()), B], dtype=torch.int64, device=device)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    red_dev = device if (not dist or args.dist_backend == "nccl") else torch.device("cpu")
+    cnt = torch.tensor([int(errs.sum()), int((errs > 0).sum()), B], dtype=torch.int64, device=red_dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     Sh.reduce_counters(cnt, tdist if dist else None)
     Sh.reduce_max(tmax, tdist if dist else None)
     elapsed = float(tmax)

@@ -77,12 +77,11 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
 /* Size the workspace for batches of up to max_batch codewords. */
 int tdec_reserve(tdec_t *h, int max_batch);
 /* Bytes of the de-punctured plane buffer for B codewords.  Layout (opaque to
- * callers): [ceil(B/64)][2][N][64] float4 -- per 64-codeword tile and trellis
- * step, {A, B, W1, Y1} and {A[perm], B[perm], W2, Y2}.  tdec_decode_planes_dev
- * completes the second vector in place (the planes are consumed). */
+ * callers): per 64-codeword tile, [N][64] float4 {A, B, W1, Y1} followed by
+ * [N][64] float2 {W2, Y2} -- 24 B per trellis step and codeword. */
 size_t tdec_planes_bytes(const tdec_t *h, int B);
 int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, float *d_planes, void *stream);
-int tdec_decode_planes_dev(tdec_t *h, int B, float *d_planes, int32_t *d_bits, double *d_lfinal,
+int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_bits, double *d_lfinal,
                            void *stream);
 int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits,
                           double *d_lfinal, void *stream);

@@ -169,10 +169,10 @@ struct tdec_ctx {
     int device = 0, N = 0, period = 1, iters = 8, algo = 0;
     uint8_t punct[16] = {0};
     long llr_len = 0, enc_len = 0;
-    bool needs_zero = false;           // punctured positions exist (planes must be zero-filled)
     int circ[16] = {0};
     int max_waves = 0;                 // resident waves of the decode kernel on this device
-    int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_dst = nullptr;
+    int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
+    int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf le, ck;                     // per-wave decode workspace
     int ws_waves = 0;
     DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
@@ -212,7 +212,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     std::memcpy(h->punct, punct, 16);
     const int N = n_couples;
     // de-puncture walk (:476-487) -> src[c*N + k] (LLR index or -1) for the 8 float4
-    // components of the tile planes (X = A, B, W1, Y1; Z = -, -, W2, Y2) and its inverse
+    // components of the tile planes (X = A, B, W1, Y1; Z = -, -, W2, Y2)
     std::vector<int32_t> src(8 * (size_t)N, -1);
     long idx = 0;
     static const int comp_of_row[4] = {2, 3, 6, 7};   // W1 -> X.z, Y1 -> X.w, W2 -> Z.z, Y2 -> Z.w
@@ -222,17 +222,18 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
         src[1 * (size_t)N + i] = (int32_t)idx++;
         for (int r = 0; r < 4; ++r) {
             if (punct[r * 4 + p]) src[comp_of_row[r] * (size_t)N + i] = (int32_t)idx++;
-            else h->needs_zero = true;
         }
     }
     h->llr_len = idx;
     h->enc_len = idx;   // encode() writes exactly what decode() reads (:449-460)
-    std::vector<int32_t> dst(idx);
-    for (int c = 0; c < 8; ++c)
-        for (int k = 0; k < N; ++k) {
-            const int j = src[(size_t)c * N + k];
-            if (j >= 0) dst[j] = (int32_t)(((c / 4) * N + k) * 4 + (c % 4));
-        }
+    std::vector<int32_t> off(N + 1);
+    for (int i = 0; i < N; ++i) off[i] = src[i];      // A of couple i is its first LLR
+    off[N] = (int32_t)idx;
+    for (int i = 0; i < N; ++i) h->max_couple_llrs = std::max(h->max_couple_llrs, off[i + 1] - off[i]);
+    if (h->max_couple_llrs > DM_MAXL / DM_KC) {   // the fused demapper's LDS tile assumes <= 6 LLRs per couple
+        delete h;
+        return fail(TDEC_EINVAL, "puncture pattern consumes more than 6 LLRs per couple");
+    }
     // encoder circular-state table: S_c = solve((I + G^N), Z) for every Z (:414-417)
     int G[16] = {0};
     G[0 * 4 + 2] = G[0 * 4 + 3] = G[1 * 4 + 0] = G[2 * 4 + 1] = G[3 * 4 + 2] = 1;
@@ -249,11 +250,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     e = hipMalloc(&h->d_perm, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
-    if (e == hipSuccess) e = hipMalloc(&h->d_dst, sizeof(int32_t) * std::max<long>(idx, 1));
+    if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
+    if (e == hipSuccess) e = hipMemcpy(h->d_off, off.data(), sizeof(int32_t) * (N + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_perm, perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_inv, inv_perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_src, src.data(), sizeof(int32_t) * 8 * N, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(h->d_dst, dst.data(), sizeof(int32_t) * idx, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     int blocks_per_cu = 0, n_cu = 0;
     if (e == hipSuccess)
@@ -276,7 +277,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_perm);
     hipFree(h->d_inv);
     hipFree(h->d_src);
-    hipFree(h->d_dst);
+    hipFree(h->d_off);
     h->le.release();
     h->ck.release();
     h->planes_own.release();
@@ -295,7 +296,7 @@ long tdec_encoded_len(const tdec_t *h) { return h ? h->enc_len : TDEC_EINVAL; }
 size_t tdec_planes_bytes(const tdec_t *h, int B) {
     if (!h || B <= 0) return 0;
     const size_t tiles = ((size_t)B + WAVE - 1) / WAVE;
-    return tiles * 2 * (size_t)h->N * WAVE * sizeof(float4);
+    return tiles * (size_t)tile_floats(h->N) * sizeof(float);
 }
 
 static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
@@ -304,7 +305,7 @@ static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
     const size_t N = h->N;
-    int rc = h->le.ensure((size_t)waves * 2 * N * WAVE * sizeof(double2));
+    int rc = h->le.ensure((size_t)waves * 3 * N * WAVE * sizeof(double2));
     if (!rc) rc = h->ck.ensure((size_t)waves * (N / WIN) * 4 * WAVE * sizeof(float4));
     if (rc) return rc;
     h->ws_waves = waves;
@@ -324,23 +325,22 @@ int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, f
     if (!h || !d_llr || !d_planes || B <= 0) return fail(TDEC_EINVAL, "bad depuncture arguments");
     if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
     Guard g(h->device);
-    const long total = (long)n_tiles_of(B) * 2 * h->N * WAVE;
+    const long total = (long)n_tiles_of(B) * h->N * WAVE;
     hipLaunchKernelGGL(k_depuncture, dim3((unsigned)((total + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                       (hipStream_t)stream, B, h->N, d_llr, llr_stride, (const int *)h->d_src, (float4 *)d_planes,
-                       total);
+                       (hipStream_t)stream, B, h->N, d_llr, llr_stride, (const int *)h->d_src, d_planes, total);
     HIPCHK(hipGetLastError());
     return 0;
 }
 
-int tdec_decode_planes_dev(tdec_t *h, int B, float *d_planes, int32_t *d_bits, double *d_lfinal,
+int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_bits, double *d_lfinal,
                            void *stream) {
     if (!h || !d_planes || !d_bits || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, (float4 *)d_planes,
-                 (double2 *)h->le.p, (float4 *)h->ck.p, d_bits, d_lfinal};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p, d_bits,
+                 d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (h->algo) hipLaunchKernelGGL(k_turbo_decode<1>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a, pm, iv);
@@ -354,7 +354,7 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
     if (!h || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
     if (B > h->cap_batch) return fail(TDEC_ECAPACITY, "batch larger than tdec_reserve()");
     int rc = tdec_depuncture_dev(h, B, d_llr, llr_stride, (float *)h->planes_own.p, stream);
-    if (!rc) rc = tdec_decode_planes_dev(h, B, (float *)h->planes_own.p, d_bits, d_lfinal, stream);
+    if (!rc) rc = tdec_decode_planes_dev(h, B, (const float *)h->planes_own.p, d_bits, d_lfinal, stream);
     return rc;
 }
 
@@ -464,20 +464,22 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     Guard g(h->device);
     hipStream_t st = (hipStream_t)stream;
     if (int rc = h->cons.upload(cons, cons_f64, M, cons_f64 != 0, st)) return rc;
-    if (h->needs_zero || (long)S * bps < h->llr_len)   // punctured / missing LLRs stay 0.0 (:469-474, :474-476)
-        HIPCHK(hipMemsetAsync(d_planes, 0, tdec_planes_bytes(h, B), st));
     DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var};
-    const long total = (long)n_tiles_of(B) * WAVE * S;
-    const dim3 grid((unsigned)((total + BLOCK - 1) / BLOCK));
+    const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
+    const int chunks = (h->N + DM_KC - 1) / DM_KC;
+    const dim3 grid((unsigned)((long)n_tiles_of(B) * chunks));
+    float *P = d_planes;
     switch (bps) {
 #define CASE(K)                                                                                              \
     case K:                                                                                                  \
         if (cons_f64)                                                                                        \
             hipLaunchKernelGGL((k_demap_planes<double, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,     \
-                               (const double *)h->cons.buf.p, c, (const int *)h->d_dst, h->llr_len, d_planes);  \
+                               (const double *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off, \
+                               n_avail, P);                                                                  \
         else                                                                                                 \
             hipLaunchKernelGGL((k_demap_planes<float, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,      \
-                               (const float *)h->cons.buf.p, c, (const int *)h->d_dst, h->llr_len, d_planes);   \
+                               (const float *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off,  \
+                               n_avail, P);                                                                  \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE

@@ -50,10 +50,9 @@ __host__ __device__ constexpr int t_prev_i(int ns, int idx) {
 // Only 16 distinct values per step: g(bA,bB,bW,bY).  g(~bits) = -g(bits)
 // exactly (round-to-nearest is sign-symmetric), so 8 are stored: index
 // bB*4 + bW*2 + bY with bA = 0.
-__device__ __forceinline__ void make_gamma(float a, float b, double laA, double laB, float w, float y,
-                                           float (&g)[8], double &inA, double &inB) {
-    inA = (double)a + laA;
-    inB = (double)b + laB;
+// Branch metrics from the channel+a-priori sums inA = f64(Lc_A) + La_A,
+// inB likewise (:135-136), and the parities (:138-139).
+__device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w, float y, float (&g)[8]) {
     const double hA = inA * 0.5, hB = inB * 0.5, hW = (double)w * 0.5, hY = (double)y * 0.5;
     const double l1[2] = {hA + hB, hA + (-hB)};
 #pragma unroll
@@ -64,6 +63,13 @@ __device__ __forceinline__ void make_gamma(float a, float b, double laA, double 
             g[bB * 4 + bW * 2 + 0] = (float)(l2 + hY);
             g[bB * 4 + bW * 2 + 1] = (float)(l2 + (-hY));
         }
+}
+
+__device__ __forceinline__ void make_gamma(float a, float b, double laA, double laB, float w, float y,
+                                           float (&g)[8], double &inA, double &inB) {
+    inA = (double)a + laA;
+    inB = (double)b + laB;
+    gamma_from_sums(inA, inB, w, y, g);
 }
 
 __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
@@ -175,22 +181,28 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
     leB = y;
 }
 
+// Element `idx` of a wave-uniform base as SGPR base + 32-bit VGPR byte offset,
+// so loads and stores use the saddr form instead of a 64-bit VGPR address.
+template <class T> __device__ __forceinline__ T &at(T *base, unsigned idx) {
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + idx * (unsigned)sizeof(T));
+}
+template <class T> __device__ __forceinline__ const T &at(const T *base, unsigned idx) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + idx * (unsigned)sizeof(T));
+}
+
 // ---- per-lane SISO --------------------------------------------------------------
-// Raw branch inputs of one trellis step: {Lc_A, Lc_B, Lc_W, Lc_Y} (f32) and the
-// a-priori {La_A, La_B} (f64).  32 B per lane, two 16-B loads.
+// Raw branch inputs of one trellis step, 32 B per lane as two 16-B loads:
+//   plain:      v = {Lc_A, Lc_B, Lc_W, Lc_Y} (f32), l = {La_A, La_B} (f64)
+//   pre-summed: v = {-, -, Lc_W, Lc_Y},          l = {inA, inB} = f64(Lc) + La
 struct Raw {
     float4 v;
     double2 l;
 };
 
-__device__ __forceinline__ void gamma_of(const Raw &r, float (&g)[8], double &iA, double &iB) {
-    make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
-}
-
-// Branch inputs of one component decoder in the tile layout: X = [N][64] float4
-// (uniform base), La = [N][64] double2 gathered through la_idx (perm / inv_perm,
-// the same index for every lane), or null for the all-zero a-priori of the
-// first iteration (:490-491).
+// Decoder 1 in the tile layout: X = [N][64] float4 {A, B, W1, Y1} (uniform
+// base), a-priori La = Le2[inv_perm[k]] ([N][64] double2, the same index for
+// every lane), or null for the all-zero a-priori of the first iteration
+// (:490-491).
 struct TileIn {
     const float4 *X;
     const double2 *La;
@@ -198,21 +210,54 @@ struct TileIn {
     int lane;
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
-        r.v = X[(long)k * WAVE + lane];
-        if (La) {
-            const long kl = la_idx ? la_idx[k] : k;
-            r.l = La[kl * WAVE + lane];
-        } else {
-            r.l = make_double2(0.0, 0.0);
-        }
+        r.v = at(X, k * WAVE + lane);
+        r.l = La ? at(La, la_idx[k] * WAVE + lane) : make_double2(0.0, 0.0);
         return r;
+    }
+    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    }
+};
+
+// Decoder 2: the sums inA = f64(Lc_A[perm[k]]) + Le1_A[perm[k]] (:511-516)
+// gathered from decoder 1's pre-summed output P1 (P1[j] = f64(Lc_A[j]) +
+// Le1_A[j], the same f64 addition), parities from Z = [N][64] float2 {W2, Y2}.
+struct TileInPre {
+    const float2 *Z;
+    const double2 *P;
+    const int *p_idx;
+    int lane;
+    __device__ __forceinline__ Raw load(int k) const {
+        Raw r;
+        const float2 z = at(Z, k * WAVE + lane);
+        r.v = make_float4(0.0f, 0.0f, z.x, z.y);
+        r.l = at(P, p_idx[k] * WAVE + lane);
+        return r;
+    }
+    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        iA = r.l.x;
+        iB = r.l.y;
+        gamma_from_sums(iA, iB, r.v.z, r.v.w, g);
+    }
+};
+
+// Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
+// iteration) Le1 itself for the final decision (:529-530).
+struct TileOutPre {
+    double2 *P, *Le;   // Le may be null
+    int lane;
+    __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
+        at(P, k * WAVE + lane) = make_double2((double)lcA + a, (double)lcB + b);
+        if (Le) at(Le, k * WAVE + lane) = make_double2(a, b);
     }
 };
 
 struct TileOut {
     double2 *Le;
     int lane;
-    __device__ __forceinline__ void store(int k, double a, double b) const { Le[(long)k * WAVE + lane] = make_double2(a, b); }
+    __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
+        at(Le, k * WAVE + lane) = make_double2(a, b);
+    }
 };
 
 // [B][N] row layout of the bcjr_max_log_map boundary (one codeword per lane).
@@ -225,12 +270,15 @@ struct RowIn {
         r.l = make_double2(LaA[k], LaB[k]);
         return r;
     }
+    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    }
 };
 
 struct RowOut {
     double *A, *B;
     bool active;
-    __device__ __forceinline__ void store(int k, double a, double b) const {
+    __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
         if (active) {
             A[k] = a;
             B[k] = b;
@@ -259,16 +307,16 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
 #pragma unroll
             for (int j = 0; j < W; ++j) {
                 double iA, iB;
-                gamma_of(raw[j], g[j], iA, iB);
+                in.gamma(raw[j], g[j], iA, iB);
             }
             if (k0 + W < N) {
 #pragma unroll
                 for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
             }
             if (pass) {
-                float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) c[q * WAVE] = make_float4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+                for (int q = 0; q < 4; ++q)
+                    at(ck, ((k0 / W) * 4 + q) * WAVE + lane) = make_float4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
             }
 #pragma unroll
             for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
@@ -285,7 +333,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             double iA, iB;
-            gamma_of(raw[j], g[j], iA, iB);
+            in.gamma(raw[j], g[j], iA, iB);
         }
         if (k0 > 0) {
 #pragma unroll
@@ -302,15 +350,18 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
     for (int k0 = N - W; k0 >= 0; k0 -= W) {
-        float gw[W][8];
+        float gw[W][8], lcA[W], lcB[W];
         double iAw[W], iBw[W];
 #pragma unroll
-        for (int j = 0; j < W; ++j) gamma_of(raw[j], gw[j], iAw[j], iBw[j]);
+        for (int j = 0; j < W; ++j) {
+            in.gamma(raw[j], gw[j], iAw[j], iBw[j]);
+            lcA[j] = raw[j].v.x;
+            lcB[j] = raw[j].v.y;
+        }
         float a0[NS];
-        const float4 *c = ck + (long)(k0 / W) * 4 * WAVE + lane;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float4 v = c[q * WAVE];
+            const float4 v = at((const float4 *)ck, ((k0 / W) * 4 + q) * WAVE + lane);
             a0[4 * q] = v.x;
             a0[4 * q + 1] = v.y;
             a0[4 * q + 2] = v.z;
@@ -333,7 +384,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, 
             for (int i = 0; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
             double leA, leB;
             extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
-            out.store(k0 + j, leA, leB);
+            out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
             beta_step<ALGO>(b, gw[j]);
         }
     }
@@ -347,13 +398,16 @@ constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 #endif
 constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval (must divide N; every table N is a multiple of 4)
 
-// Plane layout of one 64-codeword tile: [2][N][64] float4
-//   X[k] = {A[k], B[k], W1[k], Y1[k]}            decoder 1, natural order
-//   Z[k] = {A[perm[k]], B[perm[k]], W2[k], Y2[k]} decoder 2 (:507-512); .xy filled per tile
+// Plane layout of one 64-codeword tile ([N][64] each, codeword fastest):
+//   X[k] = {A[k], B[k], W1[k], Y1[k]}  float4   decoder 1, natural order
+//   Z[k] = {W2[k], Y2[k]}              float2   decoder 2's parities
+// 24 B per trellis step and codeword: exactly the de-punctured LLRs.
+__host__ __device__ constexpr long tile_floats(int N) { return (long)N * WAVE * 6; }
+
 struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
-    float4 *planes;          // [n_tiles][2][N][64]
-    double2 *le;             // [n_waves][2][N][64]: Le1, Le2 as {A, B}
+    const float *planes;     // [n_tiles] x (X, Z)
+    double2 *ws;             // [n_waves][3][N][64]: P1, Le2, Le1 (last iteration)
     float4 *ck;              // [n_waves][N/WIN][4][64]
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
@@ -364,26 +418,22 @@ template <int ALGO>
 __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int *__restrict__ perm,
                                                        const int *__restrict__ inv) {
     const int lane = threadIdx.x & (WAVE - 1);
-    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const int N = p.N;
     const long NW = (long)N * WAVE;
-    double2 *Le1 = p.le + (long)wave * 2 * NW, *Le2 = Le1 + NW;
+    double2 *P1 = p.ws + (long)wave * 3 * NW, *Le2 = P1 + NW, *Le1 = Le2 + NW;
     float4 *ck = p.ck + (long)wave * (N / WIN) * 4 * WAVE;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
-        float4 *X = p.planes + (long)tile * 2 * NW, *Z = X + NW;
-        // interleaved systematic LLRs for decoder 2 (:511-512)
-        for (int k = 0; k < N; ++k) {
-            const float4 x = X[(long)perm[k] * WAVE + lane];
-            float4 z = Z[(long)k * WAVE + lane];
-            z.x = x.x;
-            z.y = x.y;
-            Z[(long)k * WAVE + lane] = z;
-        }
+        const float *base = p.planes + (long)tile * tile_floats(N);
+        const float4 *X = reinterpret_cast<const float4 *>(base);
+        const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
-            siso<ALGO, WIN>(TileIn{X, it ? Le2 : nullptr, inv, lane}, TileOut{Le1, lane}, N, ck, lane, sf);
-            siso<ALGO, WIN>(TileIn{Z, Le1, perm, lane}, TileOut{Le2, lane}, N, ck, lane, sf);
+            const bool last = it == p.iters - 1;
+            siso<ALGO, WIN>(TileIn{X, it ? Le2 : nullptr, inv, lane}, TileOutPre{P1, last ? Le1 : nullptr, lane},
+                            N, ck, lane, sf);
+            siso<ALGO, WIN>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, lane, sf);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -416,7 +466,7 @@ struct SisoArgs {
 template <int ALGO>
 __global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
     const int lane = threadIdx.x & (WAVE - 1);
-    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const long cw = (long)wave * WAVE + lane;
     const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
@@ -425,29 +475,30 @@ __global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
     siso<ALGO, WIN>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, lane, p.sf);
 }
 
-// De-puncture (:468-487): llr rows -> tile planes X (all four) and Z (.zw only).
-// src[c*N + k] = LLR index or -1 for the 8 components c = X.xyzw, Z.xyzw
-// (Z.xy are -1 here: the decode kernel gathers them through perm).
+// De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.
+// src[c*N + k] = LLR index or -1 for the components c = X.xyzw, (unused, unused), Z.xy.
 __global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float *llr, long stride, const int *src,
-                                                     float4 *planes, long total) {
+                                                     float *planes, long total) {
     const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= total) return;                 // total = tiles * 2 * N * 64
+    if (t >= total) return;                 // total = tiles * N * 64
     const int lane = (int)(t & (WAVE - 1));
-    const long q = t >> 6;                  // (tile, half, k)
-    const long hk = q % (2L * N);
-    const long tile = q / (2L * N);
+    const long q = t >> 6;                  // (tile, k)
+    const int k = (int)(q % N);
+    const long tile = q / N;
     const long cw = tile * WAVE + lane;
-    const int half = (int)(hk / N), k = (int)(hk % N);
-    float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float v[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (cw < B) {
         const float *row = llr + cw * stride;
+        const int comp[6] = {0, 1, 2, 3, 6, 7};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int j = src[(long)(half * 4 + c) * N + k];
+        for (int c = 0; c < 6; ++c) {
+            const int j = src[(long)comp[c] * N + k];
             if (j >= 0) v[c] = row[j];
         }
     }
-    planes[t] = make_float4(v[0], v[1], v[2], v[3]);
+    float *base = planes + tile * tile_floats(N);
+    reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[4], v[5]);
 }
 
 // ---- soft demapper (compute_llr, test_sdr_with_coding.py:200-225) -----------------
@@ -478,7 +529,7 @@ struct DemapCfg {
 // All BPS LLRs of one symbol, reference sign (positive -> bit 1) unless
 // c.sign < 0.  Streams over the M points keeping a running min per bit and
 // label value, so no distance array is materialised.
-template <typename T, int BPS>
+template <typename T, int BPS, int M = (1 << BPS)>
 __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     T m0[BPS], m1[BPS];
     bool n0[BPS], n1[BPS];
@@ -487,7 +538,10 @@ __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapC
         m0[b] = m1[b] = (T)INFINITY;
         n0[b] = n1[b] = false;
     }
-    for (int m = 0; m < c.M; ++m) {
+    // M is the full label space; a table with fewer points (c.M < M) stops early.
+#pragma unroll (M <= 16 ? M : 8)
+    for (int m = 0; m < M; ++m) {
+        if (M > 2 && m >= c.M) break;
         const T a = cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
         const T v = a * a;                     // np.abs(s - constellation) ** 2
         const bool vn = v != v;
@@ -528,34 +582,67 @@ __global__ __launch_bounds__(BLOCK) void k_demap(const S *syms, long n_sym, cons
     for (int b = 0; b < BPS; ++b) llr[s * BPS + b] = v[b];
 }
 
-// Fused demap -> f32 -> de-puncture planes (the bench path).  Thread =
-// (codeword, symbol) with the codeword fastest.  dst[j] = (half*N + k)*4 + c:
-// the float4 component of the tile planes that LLR index j < n_llr feeds.
+// Fused demap -> f32 -> de-puncture planes (the bench path).
+// One block = one 64-codeword tile x DM_KC trellis steps.  Phase 1: the
+// block's threads demap every symbol covering the LLR range of those steps
+// (couples consume LLRs in order, so the range is contiguous) into an LDS
+// tile [64 codewords][range], decoder sign, rounded to f32 as decode() does
+// (:466).  Phase 2: each thread assembles whole plane entries
+// X[k] = {A, B, W1, Y1} (float4), Z[k] = {W2, Y2} (float2) and stores them
+// coalesced; punctured or missing LLRs are 0.0
+// (:469-474; the harness pads to n_coded, test_sdr_with_coding.py:474-478).
+// src[c*N + k] = LLR index of plane component c (X.xyzw, -, -, Z.xy) or -1;
+// off[k] = first LLR index of couple k (off[N] = n_llr).
+constexpr int DM_KC = 16;                  // couples per block
+constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
+constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
+
 template <typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
-                                                       DemapCfg c, const int *dst, long n_llr, float *planes) {
+                                                       DemapCfg c, const int *src, const int *off, long n_avail,
+                                                       float *planes) {
     __shared__ T cons[512];
+    __shared__ float L[WAVE * DM_LD];
     for (int i = threadIdx.x; i < 2 * c.M; i += BLOCK) cons[i] = cons_g[i];
+    const int chunks = (N + DM_KC - 1) / DM_KC;
+    const long tile = blockIdx.x / chunks;
+    const int k0 = (int)(blockIdx.x % chunks) * DM_KC;
+    const int k1 = min(N, k0 + DM_KC);
+    const long j0 = off[k0], j1 = off[k1];
+    const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
+    const int ns = (int)(s1 - s0);
     __syncthreads();
-    const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
-    const long n_tiles = (B + WAVE - 1) / WAVE;
-    if (t >= n_tiles * WAVE * S) return;
-    const int lane = (int)(t & (WAVE - 1));
-    const long q = t >> 6;
-    const long s = q % S, tile = q / S;
-    const long cw = tile * WAVE + lane;
-    if (cw >= B) return;
-    const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
-    double v[BPS];
-    sym_llrs<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-    float *P = planes + tile * 2L * N * WAVE * 4 + lane * 4;
+    for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK) {
+        const int lane = t / ns, si = t % ns;                    // consecutive threads: consecutive symbols
+        const long cw = tile * WAVE + lane;
+        const long s = s0 + si;
+        if (cw >= B || s >= S) continue;
+        const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+        double v[BPS];
+        sym_llrs<T, BPS>((T)z.x, (T)z.y, cons, c, v);
 #pragma unroll
-    for (int b = 0; b < BPS; ++b) {
-        const long j = s * BPS + b;
-        if (j < n_llr) {
-            const long d = dst[j];
-            P[(d >> 2) * WAVE * 4 + (d & 3)] = (float)v[b];   // decode(): np.array(llr, float32)
+        for (int b = 0; b < BPS; ++b) {
+            const long j = s * BPS + b;
+            if (j >= j0 && j < j1) L[lane * DM_LD + (int)(j - j0)] = (float)v[b];
         }
+    }
+    __syncthreads();
+    float *base = planes + tile * tile_floats(N);
+    for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
+        const int lane = t & (WAVE - 1);
+        const int q = t >> 6;                                    // (step, half)
+        const int k = k0 + q / 2, half = q & 1;
+        const long cw = tile * WAVE + lane;
+        const int nc = half ? 2 : 4;
+        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            if (cc >= nc) break;
+            const int j = src[(long)(half ? 6 + cc : cc) * N + k];
+            v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * DM_LD + (int)(j - j0)] : 0.0f;
+        }
+        if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+        else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
     }
 }
 

@@ -306,7 +306,7 @@ static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
     const size_t N = h->N;
     int rc = h->le.ensure((size_t)waves * 3 * N * WAVE * sizeof(double2));
-    if (!rc) rc = h->ck.ensure((size_t)waves * (N / WIN) * 4 * WAVE * sizeof(float4));
+    if (!rc) rc = h->ck.ensure((size_t)waves * (N / WIN + RING) * 4 * WAVE * sizeof(float4));
     if (rc) return rc;
     h->ws_waves = waves;
     return 0;

@@ -286,107 +286,150 @@ struct RowOut {
     }
 };
 
-// bcjr_max_log_map (:116-281) for the calling lane's codeword.
-// ck: checkpoint ring of this wave, [(N/W)][4][64] float4 (uniform base).
-// Inputs are software-pipelined one group of W steps ahead: a group's raw
-// inputs are turned into branch metrics first, then the next group's loads are
-// issued into the same registers, then the group's recursion steps run.
+// Window of the backward sweep fused with the extrinsic (:220-281): steps
+// k0+W-1 .. k0 with beta entering at position k0+W.  alpha[k] of the second
+// forward pass is recomputed from the window checkpoint (the same f32
+// operations, so bit-exact): holding all W alpha vectors of a window costs
+// 16*W VGPRs, recomputing costs W(W-1)/2 extra steps of VALU, which this
+// HBM-bound kernel has to spare.  `raw` holds the window's inputs on entry and
+// the previous window's (prefetched) on exit.
 template <int ALGO, int W, class In, class Out>
-__device__ void siso(const In &in, const Out &out, int N, float4 *ck, int lane, double sf) {
+__device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, Raw (&raw)[W], float (&b)[NS],
+                                            const float4 *ck, int lane, double sf) {
+    float gw[W][8], lcA[W], lcB[W];
+    double iAw[W], iBw[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        in.gamma(raw[j], gw[j], iAw[j], iBw[j]);
+        lcA[j] = raw[j].v.x;
+        lcB[j] = raw[j].v.y;
+    }
+    float a0[NS];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = at(ck, ((k0 / W) * 4 + q) * WAVE + lane);
+        a0[4 * q] = v.x;
+        a0[4 * q + 1] = v.y;
+        a0[4 * q + 2] = v.z;
+        a0[4 * q + 3] = v.w;
+    }
+    if (k0 > 0) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
+    }
+#pragma unroll
+    for (int j = W - 1; j >= 0; --j) {
+        __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
+        float aj[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            aj[s] = a0[s];
+            asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
+        }
+#pragma unroll
+        for (int i = 0; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
+        double leA, leB;
+        extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
+        out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
+        beta_step<ALGO>(b, gw[j]);
+    }
+}
+
+__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned base, int lane) {
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = at(c, (base + q) * WAVE + lane);
+        eq = eq && x[4 * q] == v.x && x[4 * q + 1] == v.y && x[4 * q + 2] == v.z && x[4 * q + 3] == v.w;
+    }
+    return __all(eq);
+}
+
+__device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, const float (&x)[NS]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) at(c, (base + q) * WAVE + lane) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+}
+
+// bcjr_max_log_map (:116-281) for the calling lane's codeword, 64 lanes at once.
+//
+// The reference runs each recursion twice (a convergence pass from zero, then
+// the pass it uses, started from the first pass's end state).  The two passes
+// apply the same deterministic f32 map to the same branch metrics, so once a
+// pass-2 state vector equals the pass-1 vector at the same step (IEEE ==),
+// every later one does too.  They merge after a few dozen steps (measured:
+// median 40, worst 122 of 752 at 2 dB), so pass 2 is run only until it has
+// merged in every lane of the wave:
+//   F1  alpha from 0, checkpoint alpha1 every W steps                  (:165-179)
+//   F2  alpha from alpha1[N] (:182-183), overwrite checkpoints until
+//       alpha2 == alpha1 at a checkpoint; the rest are alpha2's        (:186-197)
+//   B1  beta from 0 (:203-213) fused with a provisional extrinsic from
+//       alpha2 and beta1; beta1 kept at the first RING window starts
+//   B2  beta from beta1[0] (:216-230), recomputing the extrinsic until
+//       beta2 == beta1; below that the provisional values are exact.
+// ck: alpha checkpoints [(N/W)][4][64] float4; ring: beta1 [(RING)][4][64].
+constexpr int RING = 64;
+
+template <int ALGO, int W, class In, class Out>
+__device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, int lane, double sf) {
     Raw raw[W];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
-    // forward pass 1 (convergence, :165-179) and pass 2 (:186-197) after alpha[0] = alpha[N]
-    // (:182-183); pass 2 checkpoints alpha every W steps.
-    for (int pass = 0; pass < 2; ++pass) {
+    // F1 (inputs software-pipelined one group of W steps ahead)
 #pragma unroll
-        for (int j = 0; j < W; ++j) raw[j] = in.load(j);
-        for (int k0 = 0; k0 < N; k0 += W) {
-            float g[W][8];
-#pragma unroll
-            for (int j = 0; j < W; ++j) {
-                double iA, iB;
-                in.gamma(raw[j], g[j], iA, iB);
-            }
-            if (k0 + W < N) {
-#pragma unroll
-                for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
-            }
-            if (pass) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    at(ck, ((k0 / W) * 4 + q) * WAVE + lane) = make_float4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
-            }
-#pragma unroll
-            for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
-        }
-    }
-    // backward pass 1 (:203-213)
-    float b[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) b[s] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
-    for (int k0 = N - W; k0 >= 0; k0 -= W) {
+    for (int j = 0; j < W; ++j) raw[j] = in.load(j);
+    for (int k0 = 0; k0 < N; k0 += W) {
         float g[W][8];
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             double iA, iB;
             in.gamma(raw[j], g[j], iA, iB);
         }
-        if (k0 > 0) {
+        if (k0 + W < N) {
 #pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
+            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
         }
+        store_vec(ck, (k0 / W) * 4, lane, a);
 #pragma unroll
-        for (int j = W - 1; j >= 0; --j) beta_step<ALGO>(b, g[j]);
+        for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
     }
-    // beta[N] = beta[0] (:216-217); backward pass 2 fused with the extrinsic
-    // (:220-281).  alpha[k] of pass 2 is recomputed from the window's
-    // checkpoint (the same f32 operations, so bit-exact): holding all W alpha
-    // vectors of a window costs 16*W VGPRs, recomputing costs W(W-1)/2 extra
-    // steps per window of VALU, which this HBM-bound kernel has to spare.
+    // F2 until merged (a = alpha1[N] = alpha2[0])
+#pragma unroll
+    for (int j = 0; j < W; ++j) raw[j] = in.load(j);
+    for (int k0 = 0; k0 < N; k0 += W) {
+        if (wave_all_equal(a, ck, (k0 / W) * 4, lane)) break;
+        float g[W][8];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            double iA, iB;
+            in.gamma(raw[j], g[j], iA, iB);
+        }
+        if (k0 + W < N) {
+#pragma unroll
+            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
+        }
+        store_vec(ck, (k0 / W) * 4, lane, a);
+#pragma unroll
+        for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
+    }
+    // B1 fused with the provisional extrinsic
+    float b[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[s] = 0.0f;
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
     for (int k0 = N - W; k0 >= 0; k0 -= W) {
-        float gw[W][8], lcA[W], lcB[W];
-        double iAw[W], iBw[W];
+        const int r = (N - (k0 + W)) / W;               // window index from the top
+        if (r < RING) store_vec(ring, r * 4, lane, b);   // beta1 at position k0+W
+        back_window<ALGO, W>(in, out, k0, raw, b, ck, lane, sf);
+    }
+    // B2 until merged (b = beta1[0] = beta2[N])
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            in.gamma(raw[j], gw[j], iAw[j], iBw[j]);
-            lcA[j] = raw[j].v.x;
-            lcB[j] = raw[j].v.y;
-        }
-        float a0[NS];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = at((const float4 *)ck, ((k0 / W) * 4 + q) * WAVE + lane);
-            a0[4 * q] = v.x;
-            a0[4 * q + 1] = v.y;
-            a0[4 * q + 2] = v.z;
-            a0[4 * q + 3] = v.w;
-        }
-        if (k0 > 0) {
-#pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
-        }
-#pragma unroll
-        for (int j = W - 1; j >= 0; --j) {
-            __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
-            float aj[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                aj[s] = a0[s];
-                asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
-            }
-#pragma unroll
-            for (int i = 0; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
-            double leA, leB;
-            extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
-            out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
-            beta_step<ALGO>(b, gw[j]);
-        }
+    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
+    for (int k0 = N - W; k0 >= 0; k0 -= W) {
+        const int r = (N - (k0 + W)) / W;
+        if (r < RING && wave_all_equal(b, ring, r * 4, lane)) break;
+        back_window<ALGO, W>(in, out, k0, raw, b, ck, lane, sf);
     }
 }
 
@@ -408,7 +451,7 @@ struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
     const float *planes;     // [n_tiles] x (X, Z)
     double2 *ws;             // [n_waves][3][N][64]: P1, Le2, Le1 (last iteration)
-    float4 *ck;              // [n_waves][N/WIN][4][64]
+    float4 *ck;              // [n_waves][N/WIN + RING][4][64]: alpha checkpoints, beta1 ring
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
 };
@@ -423,7 +466,8 @@ __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int 
     const int N = p.N;
     const long NW = (long)N * WAVE;
     double2 *P1 = p.ws + (long)wave * 3 * NW, *Le2 = P1 + NW, *Le1 = Le2 + NW;
-    float4 *ck = p.ck + (long)wave * (N / WIN) * 4 * WAVE;
+    float4 *ck = p.ck + (long)wave * (N / WIN + RING) * 4 * WAVE;
+    float4 *ring = ck + (long)(N / WIN) * 4 * WAVE;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
         const float *base = p.planes + (long)tile * tile_floats(N);
         const float4 *X = reinterpret_cast<const float4 *>(base);
@@ -432,8 +476,8 @@ __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int 
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
             siso<ALGO, WIN>(TileIn{X, it ? Le2 : nullptr, inv, lane}, TileOutPre{P1, last ? Le1 : nullptr, lane},
-                            N, ck, lane, sf);
-            siso<ALGO, WIN>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, lane, sf);
+                            N, ck, ring, lane, sf);
+            siso<ALGO, WIN>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, ring, lane, sf);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -470,9 +514,10 @@ __global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
     if (wave >= p.n_waves) return;
     const long cw = (long)wave * WAVE + lane;
     const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
-    float4 *ck = p.ck + (long)wave * (p.N / WIN) * 4 * WAVE;
+    float4 *ck = p.ck + (long)wave * (p.N / WIN + RING) * 4 * WAVE;
     RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
-    siso<ALGO, WIN>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, lane, p.sf);
+    siso<ALGO, WIN>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)(p.N / WIN) * 4 * WAVE,
+                    lane, p.sf);
 }
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.

@@ -99,7 +99,7 @@ class DVBRCS2_Turbo:
         self.punct = PUNCTURE_PATTERNS[code_rate]          # KeyError for an unknown rate, as :292
         if self.N not in INTERLEAVER_PARAMS:
             raise ValueError(f"Block size {self.N} not in standard tables.")
-        self.code_rate = code_rate
+        self.rate = code_rate
         self.algo = ALGOS[algo] if isinstance(algo, str) else int(algo)
         if interleaver == "reference":
             self.perm = _t.interleaver(self.N)
@@ -236,6 +236,21 @@ class DVBRCS2_Turbo:
         _n.check(_n.lib().tdec_encode_dev(self.handle.h, B, _n.ptr(bits_u8), _n.ptr(coded_u8),
                                           _n.stream_ptr(stream)))
         return coded_u8
+
+
+class DVB_RCS2_TurboCodec(DVBRCS2_Turbo):
+    """The codec name the reference's harnesses import (turbo_test_suite.py:10,
+    test_sdr_with_coding.py:11; it no longer exists in the reference module):
+    ``DVB_RCS2_TurboCodec(block_length=, code_rate=, n_iterations=)`` with
+    ``block_length`` in couples and ``code_rate`` exposed as the float
+    k_info / n_coded that turbo_test_suite.py:133 and :221 use for the noise
+    variance.  Same decoder underneath."""
+
+    def __init__(self, block_length=212, code_rate='1/2', n_iterations=8, **kw):
+        super().__init__(block_length, code_rate, n_iterations, **kw)
+        self.block_length = block_length
+        self.n_iterations = n_iterations
+        self.code_rate = self.k_info / self.n_coded
 
 
 # ---- module-level functions of the reference ------------------------------------------

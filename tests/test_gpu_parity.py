@@ -276,3 +276,17 @@ def test_device_encoder(G_encode, n, rate):
     if f"bits_{key}" in G_encode.files:
         gb = torch.from_numpy(G_encode[f"bits_{key}"].astype(np.uint8)).cuda()
         assert np.array_equal(c.encode_device(gb).cpu().numpy(), G_encode[f"coded_{key}"])
+
+
+def test_legacy_codec_shim_decodes_like_the_codec():
+    """The BPSK AWGN recipe of turbo_test_suite.py:128-161 through the legacy name."""
+    rng = np.random.default_rng(12)
+    c = M.DVB_RCS2_TurboCodec(block_length=212, code_rate='1/3', n_iterations=8)
+    ref = M.DVBRCS2_Turbo(212, '1/3', 8)
+    snr = 10 ** (1.0 / 10)
+    nv = 1.0 / (2.0 * c.code_rate * snr)
+    for _ in range(3):
+        info = rng.integers(0, 2, c.k_info)
+        y = 1.0 - 2.0 * c.encode(info).astype(float) + np.sqrt(nv) * rng.standard_normal(c.n_coded)
+        llr = np.clip(2.0 * y / nv, -50, 50)
+        assert np.array_equal(c.decode(llr), ref.decode(llr))

@@ -82,3 +82,15 @@ def test_valid_interleaver_is_permutation():
     for n in T.INTERLEAVER_PARAMS:
         assert sorted(T.valid_interleaver(n)) == list(range(n))
         assert len(np.unique(T.interleaver(n))) < n          # the reference's is not
+
+
+def test_legacy_codec_shim():
+    """turbo_test_suite.py / test_sdr_with_coding.py construct DVB_RCS2_TurboCodec
+    with keywords and read code_rate as a float (turbo_test_suite.py:133)."""
+    c = M.DVB_RCS2_TurboCodec(block_length=212, code_rate='1/2', n_iterations=10)
+    assert c.N == 212 and c.k_info == 424 and c.n_coded == 848 and c.iterations == 10
+    assert c.code_rate == 0.5 and c.block_length == 212 and c.n_iterations == 10
+    with pytest.raises(KeyError):
+        M.DVB_RCS2_TurboCodec(block_length=212, code_rate='2/5')    # in the harness menu, not in the tables
+    with pytest.raises(ValueError):
+        M.DVB_RCS2_TurboCodec(block_length=228, code_rate='1/3')

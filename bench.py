@@ -199,6 +199,18 @@ def main():
             "ber": {"bit_errors": int(cnt[0]), "frame_errors": int(cnt[1]), "codewords": int(cnt[2]), "info_ber": int(cnt[0]) / (int(cnt[2]) * codec.k_info)},
         }
         if world == 1 and not args.no_cpu:
+            # PCIe-inclusive rate of the host-pointer drop-in boundary (DVBRCS2_Turbo.decode_batch):
+            # host f32 LLRs in, host int32 bits out, same codec and kernels (informational, never `value`)
+            hb = min(B, 131072)
+            llr_h = np.ascontiguousarray((1.0 - 2.0 * np.random.default_rng(1).integers(0, 2, (hb, codec.n_coded)))
+                                         .astype(np.float32) * 2.0)
+            codec.decode_batch(llr_h[:1024])
+            t0 = time.perf_counter()
+            codec.decode_batch(llr_h)
+            dt = time.perf_counter() - t0
+            out["host_api"] = {"value": hb / dt, "unit": "codewords/s", "batch": hb,
+                               "path": "DVBRCS2_Turbo.decode_batch(numpy f32 [B, n_coded]) -> numpy int32, "
+                                       "H2D + depuncture + decode + D2H"}
             k = min(B, 20000)
             syms_host = syms[:k].cpu().numpy()
             log("[rank 0] timing the CPU baseline (oracle) ...")

@@ -80,35 +80,35 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
 // ---- max / max* ---------------------------------------------------------------
 // log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) with the
 // historic 37 cut-off.  The correction is defined as this exact sequence of f32
-// IEEE operations (no FMA: -ffp-contract=off; correctly rounded division), the
-// same sequence the oracle restates, so log-MAP is bit-exact too.
+// IEEE operations (explicit fused multiply-adds, no division), the same
+// sequence the oracle restates, so log-MAP is bit-exact too.
 __device__ __forceinline__ float jac_corr(float d) {   // log1p(exp(-d)), 0 <= d <= 37
-    const float x0 = d * 1.44269504088896341f;
+    const float x0 = d * 0x1.715476p+0f;                     /* d * log2(e) */
     const int n = (int)x0;
     const float fn = (float)n;
-    const float r = (d - fn * 0.693145751953125f) - fn * 1.42860682030941723212e-6f;
-    const float x = -r;
-    float p = 1.0f / 40320.0f;
-    p = p * x + 1.0f / 5040.0f;
-    p = p * x + 1.0f / 720.0f;
-    p = p * x + 1.0f / 120.0f;
-    p = p * x + 1.0f / 24.0f;
-    p = p * x + 1.0f / 6.0f;
-    p = p * x + 0.5f;
-    p = p * x + 1.0f;
-    p = p * x + 1.0f;
-    const float e = ldexpf(p, -n);
-    const float u = e / (2.0f + e);
-    const float u2 = u * u;
-    float q = 1.0f / 15.0f;
-    q = q * u2 + 1.0f / 13.0f;
-    q = q * u2 + 1.0f / 11.0f;
-    q = q * u2 + 1.0f / 9.0f;
-    q = q * u2 + 1.0f / 7.0f;
-    q = q * u2 + 1.0f / 5.0f;
-    q = q * u2 + 1.0f / 3.0f;
-    q = q * u2 + 1.0f;
-    return (2.0f * u) * q;
+    float r = fmaf(-fn, 0x1.62e400p-1f, d);                   /* Cody-Waite: d - n*ln2 */
+    r = fmaf(-fn, 0x1.7f7d1cp-20f, r);
+    float p = -0x1.2755a6p-13f;                               /* exp(-r), r in [0, ln2) */
+    p = fmaf(p, r, 0x1.5c1df6p-10f);
+    p = fmaf(p, r, -0x1.0fee9ep-7f);
+    p = fmaf(p, r, 0x1.553e2ep-5f);
+    p = fmaf(p, r, -0x1.555454p-3f);
+    p = fmaf(p, r, 0x1.fffff4p-2f);
+    p = fmaf(p, r, -0x1.000000p+0f);
+    p = fmaf(p, r, 0x1.000000p+0f);
+    const float e = ldexpf(p, -n);                            /* exp(-d) */
+    float q = -0x1.2fcf46p-9f;                                /* log1p(e), e in (0, 1] */
+    q = fmaf(q, e, 0x1.f6bac6p-7f);
+    q = fmaf(q, e, -0x1.867adcp-5f);
+    q = fmaf(q, e, 0x1.871cc6p-4f);
+    q = fmaf(q, e, -0x1.2abb7cp-3f);
+    q = fmaf(q, e, 0x1.8ccddep-3f);
+    q = fmaf(q, e, -0x1.fd82a8p-3f);
+    q = fmaf(q, e, 0x1.553044p-2f);
+    q = fmaf(q, e, -0x1.fffdc0p-2f);
+    q = fmaf(q, e, 0x1.fffffap-1f);
+    q = fmaf(q, e, 0x1.c0ced2p-31f);
+    return q;
 }
 
 __device__ __forceinline__ float jac(float a, float b) {
@@ -123,6 +123,18 @@ template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {
     else return jac(m, t);
 }
 
+// acc(NEG, t): the first step of every running max*.  |NEG - t| > 37 for any
+// finite metric, so the wave skips the correction unless some lane needs it
+// (same value either way).
+template <int ALGO> __device__ __forceinline__ float acc_first(float t) {
+    if constexpr (ALGO == 0) return fmaxf(NEG, t);
+    else {
+        const float d = fabsf(NEG - t);
+        if (__all(!(d <= 37.0f))) return NEG > t ? NEG : t;
+        return jac(NEG, t);
+    }
+}
+
 template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   // max_star, :32-35
     if constexpr (ALGO == 0) return a > b ? a : b;
     else return jac(a, b);
@@ -133,9 +145,9 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
     float na[NS];
 #pragma unroll
     for (int ns = 0; ns < NS; ++ns) {
-        float m = NEG;
+        float m = acc_first<ALGO>(a[t_prev_s(ns, 0)] + gam(g, t_prev_s(ns, 0), t_prev_i(ns, 0)));
 #pragma unroll
-        for (int idx = 0; idx < 4; ++idx) {
+        for (int idx = 1; idx < 4; ++idx) {
             const int ps = t_prev_s(ns, idx), in = t_prev_i(ns, idx);
             m = acc<ALGO>(m, a[ps] + gam(g, ps, in));
         }
@@ -150,9 +162,9 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     float nb[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        float m = NEG;
+        float m = acc_first<ALGO>(b[t_next(s, 0)] + gam(g, s, 0));
 #pragma unroll
-        for (int inp = 0; inp < 4; ++inp) m = acc<ALGO>(m, b[t_next(s, inp)] + gam(g, s, inp));
+        for (int inp = 1; inp < 4; ++inp) m = acc<ALGO>(m, b[t_next(s, inp)] + gam(g, s, inp));
         nb[s] = m;
     }
     const float norm = nb[0];
@@ -163,9 +175,11 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
 template <int ALGO>
 __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)[8], const float (&b1)[NS], double inA,
                                           double inB, double sf, double &leA, double &leB) {
-    float app[4] = {NEG, NEG, NEG, NEG};
+    float app[4];
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int inp = 0; inp < 4; ++inp) app[inp] = acc_first<ALGO>((a[0] + gam(g, 0, inp)) + b1[t_next(0, inp)]);
+#pragma unroll
+    for (int s = 1; s < NS; ++s)
 #pragma unroll
         for (int inp = 0; inp < 4; ++inp) app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
     const float pA0 = star<ALGO>(app[0], app[1]), pA1 = star<ALGO>(app[2], app[3]);

@@ -95,38 +95,39 @@ static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
 /* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm
  * max(a,b) + log1p(exp(-|a-b|)), with the cut-off (|a-b| > 37 -> max) of the
  * historic _jacobian_log-22.  The correction is DEFINED as the fixed sequence of
- * f32 IEEE operations below (Cody-Waite reduction, degree-8 Taylor exp, atanh
- * series for log1p; |error| < 1e-7 against the real function), so that the
- * HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr) restates it
- * bit for bit instead of depending on two different libms. */
+ * f32 IEEE operations below -- Cody-Waite reduction, a degree-7 polynomial for
+ * exp(-r) and a degree-10 polynomial for log1p(e), all as fused multiply-adds
+ * (fmaf is correctly rounded everywhere) -- |error| < 2e-7 against the real
+ * function.  The HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr)
+ * restates it bit for bit instead of depending on two different libms. */
 static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
 {
-    const float x0 = d * 1.44269504088896341f;
+    const float x0 = d * 0x1.715476p+0f;                     /* d * log2(e) */
     const int n = (int)x0;
     const float fn = (float)n;
-    const float r = (d - fn * 0.693145751953125f) - fn * 1.42860682030941723212e-6f;
-    const float x = -r;
-    float p = 1.0f / 40320.0f;
-    p = p * x + 1.0f / 5040.0f;
-    p = p * x + 1.0f / 720.0f;
-    p = p * x + 1.0f / 120.0f;
-    p = p * x + 1.0f / 24.0f;
-    p = p * x + 1.0f / 6.0f;
-    p = p * x + 0.5f;
-    p = p * x + 1.0f;
-    p = p * x + 1.0f;
-    const float e = ldexpf(p, -n);
-    const float u = e / (2.0f + e);
-    const float u2 = u * u;
-    float q = 1.0f / 15.0f;
-    q = q * u2 + 1.0f / 13.0f;
-    q = q * u2 + 1.0f / 11.0f;
-    q = q * u2 + 1.0f / 9.0f;
-    q = q * u2 + 1.0f / 7.0f;
-    q = q * u2 + 1.0f / 5.0f;
-    q = q * u2 + 1.0f / 3.0f;
-    q = q * u2 + 1.0f;
-    return (2.0f * u) * q;
+    float r = fmaf(-fn, 0x1.62e400p-1f, d);                   /* Cody-Waite: d - n*ln2 */
+    r = fmaf(-fn, 0x1.7f7d1cp-20f, r);
+    float p = -0x1.2755a6p-13f;                               /* exp(-r), r in [0, ln2) */
+    p = fmaf(p, r, 0x1.5c1df6p-10f);
+    p = fmaf(p, r, -0x1.0fee9ep-7f);
+    p = fmaf(p, r, 0x1.553e2ep-5f);
+    p = fmaf(p, r, -0x1.555454p-3f);
+    p = fmaf(p, r, 0x1.fffff4p-2f);
+    p = fmaf(p, r, -0x1.000000p+0f);
+    p = fmaf(p, r, 0x1.000000p+0f);
+    const float e = ldexpf(p, -n);                            /* exp(-d) */
+    float q = -0x1.2fcf46p-9f;                                /* log1p(e), e in (0, 1] */
+    q = fmaf(q, e, 0x1.f6bac6p-7f);
+    q = fmaf(q, e, -0x1.867adcp-5f);
+    q = fmaf(q, e, 0x1.871cc6p-4f);
+    q = fmaf(q, e, -0x1.2abb7cp-3f);
+    q = fmaf(q, e, 0x1.8ccddep-3f);
+    q = fmaf(q, e, -0x1.fd82a8p-3f);
+    q = fmaf(q, e, 0x1.553044p-2f);
+    q = fmaf(q, e, -0x1.fffdc0p-2f);
+    q = fmaf(q, e, 0x1.fffffap-1f);
+    q = fmaf(q, e, 0x1.c0ced2p-31f);
+    return q;
 }
 
 static inline float jac(float a, float b)

@@ -307,9 +307,16 @@ struct RowOut {
 // 16*W VGPRs, recomputing costs W(W-1)/2 extra steps of VALU, which this
 // HBM-bound kernel has to spare.  `raw` holds the window's inputs on entry and
 // the previous window's (prefetched) on exit.
+#ifndef TDEC_BPF
+#define TDEC_BPF 1
+#endif
 template <int ALGO, int W, class In, class Out>
 __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, Raw (&raw)[W], float (&b)[NS],
                                             const float4 *ck, int lane, double sf) {
+    if (!TDEC_BPF) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + j);
+    }
     float gw[W][8], lcA[W], lcB[W];
     double iAw[W], iBw[W];
 #pragma unroll
@@ -327,21 +334,35 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         a0[4 * q + 2] = v.z;
         a0[4 * q + 3] = v.w;
     }
-    if (k0 > 0) {
+    if (TDEC_BPF && k0 > 0) {
 #pragma unroll
         for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
     }
+#ifndef TDEC_MID
+#define TDEC_MID 1
+#endif
+    // alpha at the window midpoint (computed once) halves the recompute: positions
+    // >= W/2 start from it, positions < W/2 from the checkpoint.
+    // (max-log only: the log-MAP instantiation, whose SISO hipcc outlines into a
+    // call, stalled on MI355X with the midpoint variant -- kept on the plain path)
+    constexpr int H = (TDEC_MID && ALGO == 0) ? W / 2 : 0;
+    float am[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) am[s] = a0[s];
+#pragma unroll
+    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
 #pragma unroll
     for (int j = W - 1; j >= 0; --j) {
         __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
+        const int from = j >= H ? H : 0;
         float aj[NS];
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            aj[s] = a0[s];
+            aj[s] = j >= H ? am[s] : a0[s];
             asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
         }
 #pragma unroll
-        for (int i = 0; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
+        for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
         double leA, leB;
         extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         out.store(k0 + j, leA, leB, lcA[j], lcB[j]);

@@ -181,9 +181,9 @@ def test_logmap_vs_oracle():
     bit-exact too (the north-star tolerance of 1e-5 is not needed)."""
     rng = np.random.default_rng(21)
     t, _ = O.trellis()
-    for n, rate, R in ((752, "1/2", 0.5), (212, "1/3", 1 / 3)):
+    for n, rate, R, B in ((752, "1/2", 0.5, 4), (212, "1/3", 1 / 3, 8)):
         c = M.DVBRCS2_Turbo(n, rate, algo="log-map")
-        _, llr = _awgn_llrs(rng, c, 12, 1.0, R)
+        _, llr = _awgn_llrs(rng, c, B, 1.0, R)
         bits, lf = c.decode_batch(llr, return_lfinal=True)
         rb, rl = O.decode_batch(llr, n, c.punct["period"], T.puncture_matrix(c.punct), 8, c.perm, c.inv_perm, t,
                                 algo=1, want_lfinal=True)

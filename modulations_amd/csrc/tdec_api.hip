@@ -163,6 +163,13 @@ int check_demap_args(int M, int bps) {
     return 0;
 }
 
+typedef void (*decode_fn)(DecodeArgs, const int *, const int *);
+
+const void *decode_kernel(int algo, bool ragged) {
+    if (algo) return ragged ? (const void *)k_turbo_decode<1, true> : (const void *)k_turbo_decode<1, false>;
+    return ragged ? (const void *)k_turbo_decode<0, true> : (const void *)k_turbo_decode<0, false>;
+}
+
 }  // namespace
 
 struct tdec_ctx {
@@ -190,7 +197,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
                 const int32_t *perm, const int32_t *inv_perm, const int32_t *tables, tdec_t **out) {
     if (!out || !punct || !perm || !inv_perm || !tables) return fail(TDEC_EINVAL, "null argument");
     *out = nullptr;
-    if (n_couples <= 0 || n_couples % WIN) return fail(TDEC_EINVAL, "n_couples must be a positive multiple of 4");
+    if (n_couples <= 0) return fail(TDEC_EINVAL, "n_couples must be positive");
     if (period < 1 || period > 4) return fail(TDEC_EINVAL, "puncture period must be 1..4");
     if (iterations < 1) return fail(TDEC_EITER, "iterations must be >= 1");
     if (algo != TDEC_ALGO_MAXLOG && algo != TDEC_ALGO_LOGMAP) return fail(TDEC_EINVAL, "unknown algorithm");
@@ -259,7 +266,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     int blocks_per_cu = 0, n_cu = 0;
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks_per_cu, algo ? (const void *)k_turbo_decode<1> : (const void *)k_turbo_decode<0>, BLOCK, 0);
+            &blocks_per_cu, decode_kernel(algo, n_couples % WIN != 0), BLOCK, 0);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
         tdec_destroy(h);
@@ -306,7 +313,7 @@ static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
     const size_t N = h->N;
     int rc = h->le.ensure((size_t)waves * 3 * N * WAVE * sizeof(double2));
-    if (!rc) rc = h->ck.ensure((size_t)waves * (N / WIN + RING) * 4 * WAVE * sizeof(float4));
+    if (!rc) rc = h->ck.ensure((size_t)waves * ((N + WIN - 1) / WIN + RING) * 4 * WAVE * sizeof(float4));
     if (rc) return rc;
     h->ws_waves = waves;
     return 0;
@@ -343,8 +350,8 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
                  d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    if (h->algo) hipLaunchKernelGGL(k_turbo_decode<1>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a, pm, iv);
-    else hipLaunchKernelGGL(k_turbo_decode<0>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a, pm, iv);
+    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % WIN != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
+                       a, pm, iv);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -401,8 +408,11 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
     SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    if (h->algo) hipLaunchKernelGGL(k_siso_batch<1>, grid, dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL(k_siso_batch<0>, grid, dim3(BLOCK), 0, s, a);
+    const bool rag = h->N % WIN != 0;
+    if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch<1, true>), grid, dim3(BLOCK), 0, s, a);
+    else if (h->algo) hipLaunchKernelGGL((k_siso_batch<1, false>), grid, dim3(BLOCK), 0, s, a);
+    else if (rag) hipLaunchKernelGGL((k_siso_batch<0, true>), grid, dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL((k_siso_batch<0, false>), grid, dim3(BLOCK), 0, s, a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(LeA, deA, nd, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(LeB, deB, nd, hipMemcpyDeviceToHost, s));

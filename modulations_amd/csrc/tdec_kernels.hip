@@ -310,12 +310,13 @@ struct RowOut {
 #ifndef TDEC_BPF
 #define TDEC_BPF 1
 #endif
-template <int ALGO, int W, class In, class Out>
-__device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, Raw (&raw)[W], float (&b)[NS],
-                                            const float4 *ck, int lane, double sf) {
+template <int ALGO, int W, bool RAG, class In, class Out>
+__device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, int len, Raw (&raw)[W],
+                                            float (&b)[NS], const float4 *ck, int lane, double sf) {
+    // len = steps in this window (W except for a ragged top window when W does not divide N)
     if (!TDEC_BPF) {
 #pragma unroll
-        for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + j);
+        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? k0 + min(j, len - 1) : k0 + j);
     }
     float gw[W][8], lcA[W], lcB[W];
     double iAw[W], iBw[W];
@@ -353,6 +354,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
     for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
 #pragma unroll
     for (int j = W - 1; j >= 0; --j) {
+        if (RAG && j >= len) continue;       // wave-uniform
         __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
         const int from = j >= H ? H : 0;
         float aj[NS];
@@ -401,18 +403,20 @@ __device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, co
 //       alpha2 and beta1; beta1 kept at the first RING window starts
 //   B2  beta from beta1[0] (:216-230), recomputing the extrinsic until
 //       beta2 == beta1; below that the provisional values are exact.
-// ck: alpha checkpoints [(N/W)][4][64] float4; ring: beta1 [(RING)][4][64].
+// ck: alpha checkpoints [ceil(N/W)][4][64] float4; ring: beta1 [RING][4][64].
+// Any N >= 1: only the top window can be short, every guard is wave-uniform.
 constexpr int RING = 64;
 
-template <int ALGO, int W, class In, class Out>
+template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, int lane, double sf) {
+    const int top = RAG ? ((N - 1) / W) * W : N - W;   // start of the (possibly short) top window
     Raw raw[W];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
     // F1 (inputs software-pipelined one group of W steps ahead)
 #pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(j);
+    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     for (int k0 = 0; k0 < N; k0 += W) {
         float g[W][8];
 #pragma unroll
@@ -422,15 +426,16 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         }
         if (k0 + W < N) {
 #pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
+            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
         store_vec(ck, (k0 / W) * 4, lane, a);
 #pragma unroll
-        for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
+        for (int j = 0; j < W; ++j)
+            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
     }
     // F2 until merged (a = alpha1[N] = alpha2[0])
 #pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(j);
+    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     for (int k0 = 0; k0 < N; k0 += W) {
         if (wave_all_equal(a, ck, (k0 / W) * 4, lane)) break;
         float g[W][8];
@@ -441,30 +446,31 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         }
         if (k0 + W < N) {
 #pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(k0 + W + j);
+            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
         store_vec(ck, (k0 / W) * 4, lane, a);
 #pragma unroll
-        for (int j = 0; j < W; ++j) alpha_step<ALGO>(a, g[j]);
+        for (int j = 0; j < W; ++j)
+            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
     }
     // B1 fused with the provisional extrinsic
     float b[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
 #pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
-    for (int k0 = N - W; k0 >= 0; k0 -= W) {
-        const int r = (N - (k0 + W)) / W;               // window index from the top
-        if (r < RING) store_vec(ring, r * 4, lane, b);   // beta1 at position k0+W
-        back_window<ALGO, W>(in, out, k0, raw, b, ck, lane, sf);
+    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+    for (int k0 = top; k0 >= 0; k0 -= W) {
+        const int r = (top - k0) / W;                     // window index from the top
+        if (r < RING) store_vec(ring, r * 4, lane, b);   // beta1 entering this window
+        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
     }
     // B2 until merged (b = beta1[0] = beta2[N])
 #pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(N - W + j);
-    for (int k0 = N - W; k0 >= 0; k0 -= W) {
-        const int r = (N - (k0 + W)) / W;
+    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+    for (int k0 = top; k0 >= 0; k0 -= W) {
+        const int r = (top - k0) / W;
         if (r < RING && wave_all_equal(b, ring, r * 4, lane)) break;
-        back_window<ALGO, W>(in, out, k0, raw, b, ck, lane, sf);
+        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
     }
 }
 
@@ -486,13 +492,13 @@ struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
     const float *planes;     // [n_tiles] x (X, Z)
     double2 *ws;             // [n_waves][3][N][64]: P1, Le2, Le1 (last iteration)
-    float4 *ck;              // [n_waves][N/WIN + RING][4][64]: alpha checkpoints, beta1 ring
+    float4 *ck;              // [n_waves][ceil(N/WIN) + RING][4][64]: alpha checkpoints, beta1 ring
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
-template <int ALGO>
+template <int ALGO, bool RAG>
 __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int *__restrict__ perm,
                                                        const int *__restrict__ inv) {
     const int lane = threadIdx.x & (WAVE - 1);
@@ -501,8 +507,9 @@ __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int 
     const int N = p.N;
     const long NW = (long)N * WAVE;
     double2 *P1 = p.ws + (long)wave * 3 * NW, *Le2 = P1 + NW, *Le1 = Le2 + NW;
-    float4 *ck = p.ck + (long)wave * (N / WIN + RING) * 4 * WAVE;
-    float4 *ring = ck + (long)(N / WIN) * 4 * WAVE;
+    const int nw = (N + WIN - 1) / WIN;
+    float4 *ck = p.ck + (long)wave * (nw + RING) * 4 * WAVE;
+    float4 *ring = ck + (long)nw * 4 * WAVE;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
         const float *base = p.planes + (long)tile * tile_floats(N);
         const float4 *X = reinterpret_cast<const float4 *>(base);
@@ -510,9 +517,9 @@ __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int 
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            siso<ALGO, WIN>(TileIn{X, it ? Le2 : nullptr, inv, lane}, TileOutPre{P1, last ? Le1 : nullptr, lane},
-                            N, ck, ring, lane, sf);
-            siso<ALGO, WIN>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, ring, lane, sf);
+            siso<ALGO, WIN, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane},
+                                 TileOutPre{P1, last ? Le1 : nullptr, lane}, N, ck, ring, lane, sf);
+            siso<ALGO, WIN, RAG>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, ring, lane, sf);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -542,17 +549,18 @@ struct SisoArgs {
     float4 *ck;
 };
 
-template <int ALGO>
+template <int ALGO, bool RAG>
 __global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const long cw = (long)wave * WAVE + lane;
     const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
-    float4 *ck = p.ck + (long)wave * (p.N / WIN + RING) * 4 * WAVE;
+    const int nw = (p.N + WIN - 1) / WIN;
+    float4 *ck = p.ck + (long)wave * (nw + RING) * 4 * WAVE;
     RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
-    siso<ALGO, WIN>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)(p.N / WIN) * 4 * WAVE,
-                    lane, p.sf);
+    siso<ALGO, WIN, RAG>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)nw * 4 * WAVE, lane,
+                         p.sf);
 }
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.

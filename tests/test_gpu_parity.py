@@ -290,3 +290,39 @@ def test_legacy_codec_shim_decodes_like_the_codec():
         y = 1.0 - 2.0 * c.encode(info).astype(float) + np.sqrt(nv) * rng.standard_normal(c.n_coded)
         llr = np.clip(2.0 * y / nv, -50, 50)
         assert np.array_equal(c.decode(llr), ref.decode(llr))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 50, 213])
+@pytest.mark.parametrize("algo", ["max-log", "log-map"])
+def test_siso_any_block_length(n, algo):
+    """bcjr_max_log_map accepts any N (the reference loops over range(N)); the
+    kernel's ragged top window must match the oracle bit for bit."""
+    rng = np.random.default_rng(n)
+    B = 70
+    Lc = (rng.standard_normal((4, B, n)) * 3).astype(np.float32)
+    La = rng.standard_normal((2, B, n)) * 6
+    t, _ = O.trellis()
+    LeA, LeB = M.bcjr_max_log_map_batch(*Lc, *La, *_tabs(), n, 0.7, algo=algo)
+    for b in range(0, B, 9):
+        rA, rB = O.siso(Lc[0, b], Lc[1, b], Lc[2, b], Lc[3, b], La[0, b], La[1, b], t, 0.7,
+                        algo=1 if algo == "log-map" else 0)
+        assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b
+
+
+def test_decode_ragged_block_length_through_c_abi():
+    """A non-table N (50 couples, own bijective interleaver) through tdec_create /
+    tdec_decode_batch: the ragged decode instantiation vs the oracle."""
+    import ctypes
+    from modulations_amd import _native as NT
+    n = 50
+    perm = ((7 * np.arange(n) + 3) % n).astype(np.int32)
+    inv = np.argsort(perm).astype(np.int32)
+    punct = T.PUNCTURE_PATTERNS["1/3"]
+    h = M._Handle(0, n, punct, 8, 0, perm, inv, T.packed_tables(*_tabs()))
+    rng = np.random.default_rng(50)
+    llr = (rng.standard_normal((65, 6 * n)) * 3).astype(np.float32)
+    bits = np.zeros((65, 2 * n), np.int32)
+    NT.check(NT.lib().tdec_decode_batch(h.h, 65, NT.ptr(llr), 6 * n, NT.ptr(bits), None))
+    t, _ = O.trellis()
+    rb = O.decode_batch(llr, n, 1, T.puncture_matrix(punct), 8, perm, inv, t)
+    assert np.array_equal(bits, rb)

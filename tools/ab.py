@@ -7,6 +7,10 @@ Each variant is loaded with its own ctypes handle (separate code objects in
 one process), fed the same device-resident planes, and timed round-robin with
 HIP events; prints median / min ms per k_turbo_decode launch and checks that
 the variants produce identical bits.
+
+Caveat (measured): the first library loaded can come out ~3% faster than a
+byte-identical copy loaded second (code-object placement), so run both orders
+before trusting a difference of that size.
 """
 import argparse
 import ctypes as C

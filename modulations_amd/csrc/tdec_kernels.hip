@@ -141,7 +141,38 @@ template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   
 }
 
 // ---- recursions -----------------------------------------------------------------
+// max-log: the two branches of a parallel pair (inputs 0/3, or 1/2: same A^B, so
+// the same next state, W and Y) leave one state for the same next state, and
+// round-to-nearest is monotone, so  max(f32(m + g), f32(m + g')) == f32(m + max(g, g'))
+// for every f32 m, g, g' (a NaN or -inf candidate is dropped either way: it can
+// never beat the -1e9 seed).  The recursions therefore add and compare once per
+// pair: pm[0][wy] = max over inputs {0, 3}, pm[1][wy] over {1, 2}, wy = 2*W + Y.
+__device__ __forceinline__ void pair_max(const float (&g)[8], float (&pm)[2][4]) {
+#pragma unroll
+    for (int wy = 0; wy < 4; ++wy) {
+        pm[0][wy] = fmaxf(g[wy], -g[3 - wy]);            // g(A0 B0 wy), g(A1 B1 wy) = -g(A0 B0 ~wy)
+        pm[1][wy] = fmaxf(g[4 + wy], -g[4 + 3 - wy]);    // g(A0 B1 wy), g(A1 B0 wy) = -g(A0 B1 ~wy)
+    }
+}
+__device__ __forceinline__ float pm_of(const float (&pm)[2][4], int s, int inp) {
+    return pm[t_dk(s, inp) ^ sb(s, 2) ^ sb(s, 3)][t_ow(s, inp) * 2 + t_oy(s, inp)];
+}
+
 template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], const float (&g)[8]) {
+    if constexpr (ALGO == 0) {
+        float pm[2][4];
+        pair_max(g, pm);
+        float na[NS];
+#pragma unroll
+        for (int ns = 0; ns < NS; ++ns) {
+            const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
+            na[ns] = fmaxf(fmaxf(NEG, a[p0] + pm_of(pm, p0, t_prev_i(ns, 0))), a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
+        }
+        const float norm = na[0];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a[s] = na[s] - norm;
+        return;
+    }
     float na[NS];
 #pragma unroll
     for (int ns = 0; ns < NS; ++ns) {
@@ -159,6 +190,18 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
 }
 
 template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], const float (&g)[8]) {
+    if constexpr (ALGO == 0) {
+        float pm[2][4];
+        pair_max(g, pm);
+        float nb[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            nb[s] = fmaxf(fmaxf(NEG, b[t_next(s, 0)] + pm_of(pm, s, 0)), b[t_next(s, 1)] + pm_of(pm, s, 1));
+        const float norm = nb[0];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
+        return;
+    }
     float nb[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {

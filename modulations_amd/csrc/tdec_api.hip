@@ -166,8 +166,8 @@ int check_demap_args(int M, int bps) {
 typedef void (*decode_fn)(DecodeArgs, const int *, const int *);
 
 const void *decode_kernel(int algo, bool ragged) {
-    if (algo) return ragged ? (const void *)k_turbo_decode<1, true> : (const void *)k_turbo_decode<1, false>;
-    return ragged ? (const void *)k_turbo_decode<0, true> : (const void *)k_turbo_decode<0, false>;
+    if (algo) return ragged ? (const void *)k_turbo_decode_logmap<true> : (const void *)k_turbo_decode_logmap<false>;
+    return ragged ? (const void *)k_turbo_decode<true> : (const void *)k_turbo_decode<false>;
 }
 
 }  // namespace
@@ -308,12 +308,15 @@ size_t tdec_planes_bytes(const tdec_t *h, int B) {
 
 static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 
+// Per-wave workspace strides (elements).
+static long ws_stride_of(const tdec_t *h) { return 3L * h->N * WAVE; }
+static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN - 1) / WIN + RING) * 4 * WAVE; }
+
 // Workspace for `waves` concurrently decoding waves.
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
-    const size_t N = h->N;
-    int rc = h->le.ensure((size_t)waves * 3 * N * WAVE * sizeof(double2));
-    if (!rc) rc = h->ck.ensure((size_t)waves * ((N + WIN - 1) / WIN + RING) * 4 * WAVE * sizeof(float4));
+    int rc = h->le.ensure((size_t)waves * ws_stride_of(h) * sizeof(double2));
+    if (!rc) rc = h->ck.ensure((size_t)waves * ck_stride_of(h) * sizeof(float4));
     if (rc) return rc;
     h->ws_waves = waves;
     return 0;
@@ -346,8 +349,8 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p, d_bits,
-                 d_lfinal};
+    DecodeArgs a{B,      h->N,      h->iters, tiles,  waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p,
+                 ws_stride_of(h), ck_stride_of(h), d_bits, d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % WIN != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
@@ -406,13 +409,13 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     HIPCHK(hipMemcpyAsync(dY, LcY, nf, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(daA, LaA, nd, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
-    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p};
+    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p, ck_stride_of(h)};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const bool rag = h->N % WIN != 0;
-    if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch<1, true>), grid, dim3(BLOCK), 0, s, a);
-    else if (h->algo) hipLaunchKernelGGL((k_siso_batch<1, false>), grid, dim3(BLOCK), 0, s, a);
-    else if (rag) hipLaunchKernelGGL((k_siso_batch<0, true>), grid, dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL((k_siso_batch<0, false>), grid, dim3(BLOCK), 0, s, a);
+    if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
+    else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
+    else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(LeA, deA, nd, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(LeB, deB, nd, hipMemcpyDeviceToHost, s));

@@ -141,6 +141,7 @@ template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   
 }
 
 // ---- recursions -----------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32: two IEEE f32 adds per lane
 // max-log: the two branches of a parallel pair (inputs 0/3, or 1/2: same A^B, so
 // the same next state, W and Y) leave one state for the same next state, and
 // round-to-nearest is monotone, so  max(f32(m + g), f32(m + g')) == f32(m + max(g, g'))
@@ -158,19 +159,43 @@ __device__ __forceinline__ float pm_of(const float (&pm)[2][4], int s, int inp) 
     return pm[t_dk(s, inp) ^ sb(s, 2) ^ sb(s, 3)][t_ow(s, inp) * 2 + t_oy(s, inp)];
 }
 
+// The adds run two per v_pk_add_f32.  Register pairs: alpha {a[q], a[q+8]} (the two
+// predecessors of a state), beta {b[2m], b[2m+1]} (the two successors of a state),
+// and PM[t][wy] = {pm[t][wy], pm[1-t][3-wy]}: the two pair maxima one state's two
+// branch pairs use (the other pair flips A^B, and with it W and Y).
+__device__ __forceinline__ void pair_max2(const float (&g)[8], f2 (&P)[4]) {
+#pragma unroll
+    for (int wy = 0; wy < 4; ++wy)   // P[wy] = {pm[0][wy], pm[1][3-wy]}
+        P[wy] = f2{fmaxf(g[wy], -g[3 - wy]), fmaxf(g[4 + 3 - wy], -g[4 + wy])};
+}
+// x + PM[t][wy], PM[t][wy] = {pm[t][wy], pm[1-t][3-wy]}: P[wy] for t = 0, and for
+// t = 1 P[3-wy] with its halves swapped by the instruction's operand select
+__device__ __forceinline__ f2 add_PM(f2 x, const f2 (&P)[4], int s, int inp) {
+    const int t = t_dk(s, inp) ^ sb(s, 2) ^ sb(s, 3), wy = t_ow(s, inp) * 2 + t_oy(s, inp);
+    if (t == 0) return x + P[wy];
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(x), "v"(P[3 - wy]));
+    return r;
+}
+
 template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], const float (&g)[8]) {
     if constexpr (ALGO == 0) {
-        float pm[2][4];
-        pair_max(g, pm);
+        f2 PM[4];
+        pair_max2(g, PM);
         float na[NS];
 #pragma unroll
         for (int ns = 0; ns < NS; ++ns) {
-            const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
-            na[ns] = fmaxf(fmaxf(NEG, a[p0] + pm_of(pm, p0, t_prev_i(ns, 0))), a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
+            const int p0 = t_prev_s(ns, 0);   // the other predecessor is p0 + 8
+            const f2 t = add_PM(f2{a[p0], a[p0 + 8]}, PM, p0, t_prev_i(ns, 0));
+            na[ns] = fmaxf(fmaxf(NEG, t.x), t.y);
         }
         const float norm = na[0];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) a[s] = na[s] - norm;
+        for (int s = 0; s < NS / 2; ++s) {
+            const f2 v = f2{na[s], na[s + 8]} - f2{norm, norm};
+            a[s] = v.x;
+            a[s + 8] = v.y;
+        }
         return;
     }
     float na[NS];
@@ -191,15 +216,23 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
 
 template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], const float (&g)[8]) {
     if constexpr (ALGO == 0) {
-        float pm[2][4];
-        pair_max(g, pm);
+        f2 PM[4];
+        pair_max2(g, PM);
         float nb[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s)
-            nb[s] = fmaxf(fmaxf(NEG, b[t_next(s, 0)] + pm_of(pm, s, 0)), b[t_next(s, 1)] + pm_of(pm, s, 1));
+        for (int s = 0; s < NS; ++s) {
+            const int ie = (t_next(s, 0) & 1) ? 1 : 0;   // the input going to the even successor
+            const int n = t_next(s, ie);
+            const f2 t = add_PM(f2{b[n], b[n + 1]}, PM, s, ie);
+            nb[s] = fmaxf(fmaxf(NEG, t.x), t.y);
+        }
         const float norm = nb[0];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
+        for (int s = 0; s < NS; s += 2) {
+            const f2 v = f2{nb[s], nb[s + 1]} - f2{norm, norm};
+            b[s] = v.x;
+            b[s + 1] = v.y;
+        }
         return;
     }
     float nb[NS];
@@ -215,16 +248,61 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
 }
 
+// {x[H] + G.lo, x[H] - G.hi} (SW = 0) or {x[H] + G.hi, x[H] - G.lo} (SW = 1)
+template <int H, int SW> __device__ __forceinline__ f2 pk_bcast_add_gpair(f2 x, f2 G) {
+    f2 r;
+    if constexpr (H == 0 && SW == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(G));
+    if constexpr (H == 1 && SW == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(G));
+    if constexpr (H == 0 && SW == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(G));
+    if constexpr (H == 1 && SW == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(G));
+    return r;
+}
+// {t.lo + y[E], t.hi + y[E]}
+template <int E> __device__ __forceinline__ f2 pk_add_bcast(f2 t, f2 y) {
+    f2 r;
+    if constexpr (E == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(r) : "v"(t), "v"(y));
+    else asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(t), "v"(y));
+    return r;
+}
+
 template <int ALGO>
 __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)[8], const float (&b1)[NS], double inA,
                                           double inB, double sf, double &leA, double &leB) {
     float app[4];
+    if constexpr (ALGO == 0) {
+        // (a[s] + gamma) + beta for the two inputs of a parallel pair (same next
+        // state) in one lane-pair: gamma pair {g(A B wy), g(~A ~B wy)} = {g[i], -g[j]}
+        // from the register pairs GP = {g0,g3}, {g1,g2}, {g4,g7}, {g5,g6}.
+        const f2 GP[4] = {f2{g[0], g[3]}, f2{g[1], g[2]}, f2{g[4], g[7]}, f2{g[5], g[6]}};
 #pragma unroll
-    for (int inp = 0; inp < 4; ++inp) app[inp] = acc_first<ALGO>((a[0] + gam(g, 0, inp)) + b1[t_next(0, inp)]);
+        for (int i = 0; i < 4; ++i) app[i] = NEG;
 #pragma unroll
-    for (int s = 1; s < NS; ++s)
+        for (int s = 0; s < NS; ++s) {
+            const f2 A2 = f2{a[s & 7], a[(s & 7) + 8]};
 #pragma unroll
-        for (int inp = 0; inp < 4; ++inp) app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
+            for (int T = 0; T < 2; ++T) {
+                const int lo = T ? 1 : 0, hi = lo ^ 3;              // inputs {0, 3} or {1, 2}
+                const int wy = t_ow(s, lo) * 2 + t_oy(s, lo);
+                const int gi = 2 * T + (wy < 2 ? wy : 3 - wy);
+                const int ns = t_next(s, lo);
+                const f2 B2 = f2{b1[ns & ~1], b1[ns | 1]};
+                f2 u;
+                if (s < 8) u = wy < 2 ? pk_bcast_add_gpair<0, 0>(A2, GP[gi]) : pk_bcast_add_gpair<0, 1>(A2, GP[gi]);
+                else u = wy < 2 ? pk_bcast_add_gpair<1, 0>(A2, GP[gi]) : pk_bcast_add_gpair<1, 1>(A2, GP[gi]);
+                const f2 t = (ns & 1) ? pk_add_bcast<1>(u, B2) : pk_add_bcast<0>(u, B2);
+                app[lo] = fmaxf(app[lo], t.x);
+                app[hi] = fmaxf(app[hi], t.y);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int inp = 0; inp < 4; ++inp) app[inp] = acc_first<ALGO>((a[0] + gam(g, 0, inp)) + b1[t_next(0, inp)]);
+#pragma unroll
+        for (int s = 1; s < NS; ++s)
+#pragma unroll
+            for (int inp = 0; inp < 4; ++inp)
+                app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
+    }
     const float pA0 = star<ALGO>(app[0], app[1]), pA1 = star<ALGO>(app[2], app[3]);
     const float pB0 = star<ALGO>(app[0], app[2]), pB1 = star<ALGO>(app[1], app[3]);
     const float LpA = pA0 - pA1, LpB = pB0 - pB1;
@@ -343,6 +421,43 @@ struct RowOut {
     }
 };
 
+// Stored element order of a state vector: alpha vectors (ALPHA) in their register
+// pairs {a[q], a[q+8]}, so float4 #c = {a[2c], a[2c+8], a[2c+1], a[2c+9]}; beta
+// vectors in natural order (their pairs {b[2m], b[2m+1]} are already adjacent).
+template <bool ALPHA> __device__ __forceinline__ constexpr int vec_elem(int c, int e) {
+    return ALPHA ? 2 * c + (e >> 1) + 8 * (e & 1) : 4 * c + e;
+}
+
+template <bool ALPHA> __device__ __forceinline__ void load_vec(float (&x)[NS], const float4 *c, unsigned base, int lane) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = at(c, (base + q) * WAVE + lane);
+        x[vec_elem<ALPHA>(q, 0)] = v.x;
+        x[vec_elem<ALPHA>(q, 1)] = v.y;
+        x[vec_elem<ALPHA>(q, 2)] = v.z;
+        x[vec_elem<ALPHA>(q, 3)] = v.w;
+    }
+}
+
+template <bool ALPHA>
+__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned base, int lane) {
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = at(c, (base + q) * WAVE + lane);
+        eq = eq && x[vec_elem<ALPHA>(q, 0)] == v.x && x[vec_elem<ALPHA>(q, 1)] == v.y &&
+             x[vec_elem<ALPHA>(q, 2)] == v.z && x[vec_elem<ALPHA>(q, 3)] == v.w;
+    }
+    return __all(eq);
+}
+
+template <bool ALPHA> __device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, const float (&x)[NS]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        at(c, (base + q) * WAVE + lane) = make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
+                                                      x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]);
+}
+
 // Window of the backward sweep fused with the extrinsic (:220-281): steps
 // k0+W-1 .. k0 with beta entering at position k0+W.  alpha[k] of the second
 // forward pass is recomputed from the window checkpoint (the same f32
@@ -370,14 +485,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         lcB[j] = raw[j].v.y;
     }
     float a0[NS];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float4 v = at(ck, ((k0 / W) * 4 + q) * WAVE + lane);
-        a0[4 * q] = v.x;
-        a0[4 * q + 1] = v.y;
-        a0[4 * q + 2] = v.z;
-        a0[4 * q + 3] = v.w;
-    }
+    load_vec<true>(a0, ck, (k0 / W) * 4, lane);
     if (TDEC_BPF && k0 > 0) {
 #pragma unroll
         for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
@@ -415,21 +523,6 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
     }
 }
 
-__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned base, int lane) {
-    bool eq = true;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float4 v = at(c, (base + q) * WAVE + lane);
-        eq = eq && x[4 * q] == v.x && x[4 * q + 1] == v.y && x[4 * q + 2] == v.z && x[4 * q + 3] == v.w;
-    }
-    return __all(eq);
-}
-
-__device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, const float (&x)[NS]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) at(c, (base + q) * WAVE + lane) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-}
-
 // bcjr_max_log_map (:116-281) for the calling lane's codeword, 64 lanes at once.
 //
 // The reference runs each recursion twice (a convergence pass from zero, then
@@ -443,12 +536,14 @@ __device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, co
 //   F2  alpha from alpha1[N] (:182-183), overwrite checkpoints until
 //       alpha2 == alpha1 at a checkpoint; the rest are alpha2's        (:186-197)
 //   B1  beta from 0 (:203-213) fused with a provisional extrinsic from
-//       alpha2 and beta1; beta1 kept at the first RING window starts
+//       alpha2 and beta1; beta1 kept at every RSTEP-th of the first
+//       RING*RSTEP window starts
 //   B2  beta from beta1[0] (:216-230), recomputing the extrinsic until
-//       beta2 == beta1; below that the provisional values are exact.
+//       beta2 == beta1 at a kept window start; below that the provisional
+//       values are exact (a pass that has not merged by then runs to the end).
 // ck: alpha checkpoints [ceil(N/W)][4][64] float4; ring: beta1 [RING][4][64].
 // Any N >= 1: only the top window can be short, every guard is wave-uniform.
-constexpr int RING = 64;
+constexpr int RING = 16, RSTEP = 4;   // beta1 kept over the top 256 steps (merge: median 40, max 122)
 
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, int lane, double sf) {
@@ -471,7 +566,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
-        store_vec(ck, (k0 / W) * 4, lane, a);
+        store_vec<true>(ck, (k0 / W) * 4, lane, a);
 #pragma unroll
         for (int j = 0; j < W; ++j)
             if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
@@ -480,7 +575,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     for (int k0 = 0; k0 < N; k0 += W) {
-        if (wave_all_equal(a, ck, (k0 / W) * 4, lane)) break;
+        if (wave_all_equal<true>(a, ck, (k0 / W) * 4, lane)) break;
         float g[W][8];
 #pragma unroll
         for (int j = 0; j < W; ++j) {
@@ -491,7 +586,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
-        store_vec(ck, (k0 / W) * 4, lane, a);
+        store_vec<true>(ck, (k0 / W) * 4, lane, a);
 #pragma unroll
         for (int j = 0; j < W; ++j)
             if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
@@ -504,7 +599,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;                     // window index from the top
-        if (r < RING) store_vec(ring, r * 4, lane, b);   // beta1 entering this window
+        if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, r / RSTEP * 4, lane, b);   // beta1 entering
         back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
     }
     // B2 until merged (b = beta1[0] = beta2[N])
@@ -512,7 +607,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;
-        if (r < RING && wave_all_equal(b, ring, r * 4, lane)) break;
+        if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, r / RSTEP * 4, lane)) break;
         back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
     }
 }
@@ -534,24 +629,25 @@ __host__ __device__ constexpr long tile_floats(int N) { return (long)N * WAVE * 
 struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
     const float *planes;     // [n_tiles] x (X, Z)
-    double2 *ws;             // [n_waves][3][N][64]: P1, Le2, Le1 (last iteration)
-    float4 *ck;              // [n_waves][ceil(N/WIN) + RING][4][64]: alpha checkpoints, beta1 ring
+    double2 *ws;             // [n_waves] x ws_stride: [3][N][64] P1, Le2, Le1 (last iteration)
+    float4 *ck;              // [n_waves] x ck_stride: [ceil(N/WIN) + RING][4][64] alpha checkpoints, beta1 ring
+    long ws_stride, ck_stride;   // per-wave strides (elements)
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
 template <int ALGO, bool RAG>
-__global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int *__restrict__ perm,
-                                                       const int *__restrict__ inv) {
+__device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
+                                                   const int *__restrict__ inv) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const int N = p.N;
     const long NW = (long)N * WAVE;
-    double2 *P1 = p.ws + (long)wave * 3 * NW, *Le2 = P1 + NW, *Le1 = Le2 + NW;
+    double2 *P1 = p.ws + (long)wave * p.ws_stride, *Le2 = P1 + NW, *Le1 = Le2 + NW;
     const int nw = (N + WIN - 1) / WIN;
-    float4 *ck = p.ck + (long)wave * (nw + RING) * 4 * WAVE;
+    float4 *ck = p.ck + (long)wave * p.ck_stride;
     float4 *ring = ck + (long)nw * 4 * WAVE;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
         const float *base = p.planes + (long)tile * tile_floats(N);
@@ -582,6 +678,20 @@ __global__ __launch_bounds__(BLOCK) void k_turbo_decode(DecodeArgs p, const int 
     }
 }
 
+// max-log: held to 256 registers (2 waves per SIMD; the few tile-level values that
+// do not fit go to scratch, outside the trellis loops).  log-MAP keeps the
+// compiler's own budget (its max* needs the registers: 1 wave per SIMD).
+template <bool RAG>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_turbo_decode(
+    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
+    turbo_decode_tiles<0, RAG>(p, perm, inv);
+}
+template <bool RAG>
+__global__ __launch_bounds__(BLOCK) void k_turbo_decode_logmap(DecodeArgs p, const int *__restrict__ perm,
+                                                              const int *__restrict__ inv) {
+    turbo_decode_tiles<1, RAG>(p, perm, inv);
+}
+
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).
 struct SisoArgs {
     int B, N, n_waves;
@@ -590,20 +700,27 @@ struct SisoArgs {
     double sf;
     double *LeA, *LeB;
     float4 *ck;
+    long ck_stride;
 };
 
-template <int ALGO, bool RAG>
-__global__ __launch_bounds__(BLOCK) void k_siso_batch(SisoArgs p) {
+template <int ALGO, bool RAG> __device__ __forceinline__ void siso_rows(const SisoArgs &p) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const long cw = (long)wave * WAVE + lane;
     const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
     const int nw = (p.N + WIN - 1) / WIN;
-    float4 *ck = p.ck + (long)wave * (nw + RING) * 4 * WAVE;
+    float4 *ck = p.ck + (long)wave * p.ck_stride;
     RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
     siso<ALGO, WIN, RAG>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)nw * 4 * WAVE, lane,
                          p.sf);
+}
+template <bool RAG>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_siso_batch(SisoArgs p) {
+    siso_rows<0, RAG>(p);
+}
+template <bool RAG> __global__ __launch_bounds__(BLOCK) void k_siso_batch_logmap(SisoArgs p) {
+    siso_rows<1, RAG>(p);
 }
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.

@@ -17,7 +17,7 @@ import sys
 
 
 def short(name):
-    for k in ("k_turbo_decode", "k_demap_planes", "k_depuncture", "k_encode", "k_siso_batch", "k_demap"):
+    for k in ("k_turbo_decode_logmap", "k_turbo_decode", "k_demap_planes", "k_depuncture", "k_encode", "k_siso_batch", "k_demap"):
         if k in name:
             return k
     return name[:60]
@@ -60,20 +60,26 @@ def main(src, dst, batch=1 << 20):
             d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
         if "SQ_WAVE_CYCLES" in c:
             d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            d["wait_inst_any_frac"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+            d["active_inst_any_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
             d["valu_insts_per_codeword"] = c.get("SQ_INSTS_VALU", 0) * 64 / batch
-            # VALU issue-busy share: wave-instructions x 2 cycles (SIMD-32) / (1024 SIMDs x cycles)
+            # clock from GRBM_GUI_ACTIVE (summed over the 8 XCDs)
+            clk = 2.4e9
             if "GRBM_GUI_ACTIVE" in c:
-                pass
-            d["valu_busy_est"] = c.get("SQ_INSTS_VALU", 0) * 2 / (1024 * 2.4e9 * d["avg_ms"] * 1e-3)
+                clk = c["GRBM_GUI_ACTIVE"] / 8 / (d["avg_ms"] * 1e-3)
+                d["clock_GHz"] = clk / 1e9
+            # VALU issue-busy share: wave-instructions x 2 cycles (SIMD-32) / (1024 SIMDs x cycles)
+            d["valu_busy_est"] = c.get("SQ_INSTS_VALU", 0) * 2 / (1024 * clk * d["avg_ms"] * 1e-3)
     json.dump(out, open(dst + "_summary.json", "w"), indent=1)
     with open(dst + "_summary.md", "w") as f:
         f.write(f"# rocprofv3 summary ({src}), batch = {batch} codewords\n\n")
-        f.write("| kernel | calls | avg ms | HBM GB/launch | HBM GB/s | B/codeword | L2 hit | VALU busy (est) | wait_any |\n")
-        f.write("|---|---|---|---|---|---|---|---|---|\n")
+        f.write("| kernel | calls | avg ms | HBM GB/launch | HBM GB/s | B/codeword | L2 hit | VALU busy (est) | wait_any | wait_inst | clock GHz |\n")
+        f.write("|---|---|---|---|---|---|---|---|---|---|---|\n")
         for k, d in out["kernels"].items():
             f.write(f"| {k} | {d['calls']} | {d['avg_ms']:.2f} | {d.get('hbm_bytes_per_launch', 0) / 1e9:.1f} | "
                     f"{d.get('hbm_GBps', 0):.0f} | {d.get('hbm_bytes_per_codeword', 0):.0f} | "
-                    f"{d.get('l2_hit_rate', 0):.2f} | {d.get('valu_busy_est', 0):.2f} | {d.get('wait_any_frac', 0):.2f} |\n")
+                    f"{d.get('l2_hit_rate', 0):.2f} | {d.get('valu_busy_est', 0):.2f} | {d.get('wait_any_frac', 0):.2f} | "
+                    f"{d.get('wait_inst_any_frac', 0):.2f} | {d.get('clock_GHz', 0):.2f} |\n")
     print(open(dst + "_summary.md").read())
 
 

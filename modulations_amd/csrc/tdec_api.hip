@@ -273,6 +273,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
         return fail(TDEC_EHIP, std::string("tdec_create: ") + hipGetErrorString(e));
     }
     h->max_waves = std::max(1, blocks_per_cu) * n_cu * WAVES_PER_BLOCK;
+    // the kernels address one workspace plane / the checkpoint array with 32-bit
+    // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
+    const long row_units = std::max<long>(N, 4L * ((N + WIN - 1) / WIN + RING));
+    const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
+    h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
     *out = h;
     return TDEC_OK;
 }
@@ -349,8 +354,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B,      h->N,      h->iters, tiles,  waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p,
-                 ws_stride_of(h), ck_stride_of(h), d_bits, d_lfinal};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p, d_bits, d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % WIN != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,

@@ -343,10 +343,11 @@ struct TileIn {
     const double2 *La;
     const int *la_idx;
     int lane;
+    unsigned rs;   // workspace row stride (elements between trellis steps)
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
         r.v = at(X, k * WAVE + lane);
-        r.l = La ? at(La, la_idx[k] * WAVE + lane) : make_double2(0.0, 0.0);
+        r.l = La ? at(La, la_idx[k] * rs + lane) : make_double2(0.0, 0.0);
         return r;
     }
     __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
@@ -362,11 +363,12 @@ struct TileInPre {
     const double2 *P;
     const int *p_idx;
     int lane;
+    unsigned rs;
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
         const float2 z = at(Z, k * WAVE + lane);
         r.v = make_float4(0.0f, 0.0f, z.x, z.y);
-        r.l = at(P, p_idx[k] * WAVE + lane);
+        r.l = at(P, p_idx[k] * rs + lane);
         return r;
     }
     __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
@@ -381,17 +383,19 @@ struct TileInPre {
 struct TileOutPre {
     double2 *P, *Le;   // Le may be null
     int lane;
+    unsigned rs;
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
-        at(P, k * WAVE + lane) = make_double2((double)lcA + a, (double)lcB + b);
-        if (Le) at(Le, k * WAVE + lane) = make_double2(a, b);
+        at(P, k * rs + lane) = make_double2((double)lcA + a, (double)lcB + b);
+        if (Le) at(Le, k * rs + lane) = make_double2(a, b);
     }
 };
 
 struct TileOut {
     double2 *Le;
     int lane;
+    unsigned rs;
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
-        at(Le, k * WAVE + lane) = make_double2(a, b);
+        at(Le, k * rs + lane) = make_double2(a, b);
     }
 };
 
@@ -428,10 +432,12 @@ template <bool ALPHA> __device__ __forceinline__ constexpr int vec_elem(int c, i
     return ALPHA ? 2 * c + (e >> 1) + 8 * (e & 1) : 4 * c + e;
 }
 
-template <bool ALPHA> __device__ __forceinline__ void load_vec(float (&x)[NS], const float4 *c, unsigned base, int lane) {
+// c: slot base of the calling wave, cs: elements between consecutive float4 slots
+template <bool ALPHA>
+__device__ __forceinline__ void load_vec(float (&x)[NS], const float4 *c, unsigned cs, unsigned base, int lane) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const float4 v = at(c, (base + q) * WAVE + lane);
+        const float4 v = at(c, (base + q) * cs + lane);
         x[vec_elem<ALPHA>(q, 0)] = v.x;
         x[vec_elem<ALPHA>(q, 1)] = v.y;
         x[vec_elem<ALPHA>(q, 2)] = v.z;
@@ -440,21 +446,23 @@ template <bool ALPHA> __device__ __forceinline__ void load_vec(float (&x)[NS], c
 }
 
 template <bool ALPHA>
-__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned base, int lane) {
+__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned cs, unsigned base,
+                                               int lane) {
     bool eq = true;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const float4 v = at(c, (base + q) * WAVE + lane);
+        const float4 v = at(c, (base + q) * cs + lane);
         eq = eq && x[vec_elem<ALPHA>(q, 0)] == v.x && x[vec_elem<ALPHA>(q, 1)] == v.y &&
              x[vec_elem<ALPHA>(q, 2)] == v.z && x[vec_elem<ALPHA>(q, 3)] == v.w;
     }
     return __all(eq);
 }
 
-template <bool ALPHA> __device__ __forceinline__ void store_vec(float4 *c, unsigned base, int lane, const float (&x)[NS]) {
+template <bool ALPHA>
+__device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base, int lane, const float (&x)[NS]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        at(c, (base + q) * WAVE + lane) = make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
+        at(c, (base + q) * cs + lane) = make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
                                                       x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]);
 }
 
@@ -470,7 +478,7 @@ template <bool ALPHA> __device__ __forceinline__ void store_vec(float4 *c, unsig
 #endif
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, int len, Raw (&raw)[W],
-                                            float (&b)[NS], const float4 *ck, int lane, double sf) {
+                                            float (&b)[NS], const float4 *ck, unsigned cs, int lane, double sf) {
     // len = steps in this window (W except for a ragged top window when W does not divide N)
     if (!TDEC_BPF) {
 #pragma unroll
@@ -485,7 +493,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         lcB[j] = raw[j].v.y;
     }
     float a0[NS];
-    load_vec<true>(a0, ck, (k0 / W) * 4, lane);
+    load_vec<true>(a0, ck, cs, (k0 / W) * 4, lane);
     if (TDEC_BPF && k0 > 0) {
 #pragma unroll
         for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
@@ -546,7 +554,8 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 constexpr int RING = 16, RSTEP = 4;   // beta1 kept over the top 256 steps (merge: median 40, max 122)
 
 template <int ALGO, int W, bool RAG, class In, class Out>
-__device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, int lane, double sf) {
+__device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane,
+                     double sf) {
     const int top = RAG ? ((N - 1) / W) * W : N - W;   // start of the (possibly short) top window
     Raw raw[W];
     float a[NS];
@@ -566,7 +575,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
-        store_vec<true>(ck, (k0 / W) * 4, lane, a);
+        store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
 #pragma unroll
         for (int j = 0; j < W; ++j)
             if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
@@ -575,7 +584,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     for (int k0 = 0; k0 < N; k0 += W) {
-        if (wave_all_equal<true>(a, ck, (k0 / W) * 4, lane)) break;
+        if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
         float g[W][8];
 #pragma unroll
         for (int j = 0; j < W; ++j) {
@@ -586,7 +595,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
         }
-        store_vec<true>(ck, (k0 / W) * 4, lane, a);
+        store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
 #pragma unroll
         for (int j = 0; j < W; ++j)
             if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
@@ -599,16 +608,16 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;                     // window index from the top
-        if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, r / RSTEP * 4, lane, b);   // beta1 entering
-        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
+        if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
+        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
     }
     // B2 until merged (b = beta1[0] = beta2[N])
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;
-        if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, r / RSTEP * 4, lane)) break;
-        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, lane, sf);
+        if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
+        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
     }
 }
 
@@ -629,9 +638,8 @@ __host__ __device__ constexpr long tile_floats(int N) { return (long)N * WAVE * 
 struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
     const float *planes;     // [n_tiles] x (X, Z)
-    double2 *ws;             // [n_waves] x ws_stride: [3][N][64] P1, Le2, Le1 (last iteration)
-    float4 *ck;              // [n_waves] x ck_stride: [ceil(N/WIN) + RING][4][64] alpha checkpoints, beta1 ring
-    long ws_stride, ck_stride;   // per-wave strides (elements)
+    double2 *ws;             // [3][N][n_waves][64]: P1, Le2, Le1 (last iteration)
+    float4 *ck;              // [ceil(N/WIN) + RING][4][n_waves][64]: alpha checkpoints, beta1 ring
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
 };
@@ -645,10 +653,12 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     if (wave >= p.n_waves) return;
     const int N = p.N;
     const long NW = (long)N * WAVE;
-    double2 *P1 = p.ws + (long)wave * p.ws_stride, *Le2 = P1 + NW, *Le1 = Le2 + NW;
+    // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
+    const unsigned rs = (unsigned)p.n_waves * WAVE;
+    double2 *P1 = p.ws + (long)wave * WAVE, *Le2 = P1 + (long)N * rs, *Le1 = Le2 + (long)N * rs;
     const int nw = (N + WIN - 1) / WIN;
-    float4 *ck = p.ck + (long)wave * p.ck_stride;
-    float4 *ring = ck + (long)nw * 4 * WAVE;
+    float4 *ck = p.ck + (long)wave * WAVE;
+    float4 *ring = ck + (long)nw * 4 * rs;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
         const float *base = p.planes + (long)tile * tile_floats(N);
         const float4 *X = reinterpret_cast<const float4 *>(base);
@@ -656,9 +666,9 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            siso<ALGO, WIN, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane},
-                                 TileOutPre{P1, last ? Le1 : nullptr, lane}, N, ck, ring, lane, sf);
-            siso<ALGO, WIN, RAG>(TileInPre{Z, P1, perm, lane}, TileOut{Le2, lane}, N, ck, ring, lane, sf);
+            siso<ALGO, WIN, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
+                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs}, N, ck, ring, rs, lane, sf);
+            siso<ALGO, WIN, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -667,8 +677,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
             for (int k = 0; k < N; ++k) {
                 const float4 x = X[(long)k * WAVE + lane];
-                const double2 la = Le2[(long)inv[k] * WAVE + lane];
-                const double2 le = Le1[(long)k * WAVE + lane];
+                const double2 la = Le2[(long)inv[k] * rs + lane];
+                const double2 le = Le1[(long)k * rs + lane];
                 const double fa = ((double)x.x + la.x) + le.x;
                 const double fb = ((double)x.y + la.y) + le.y;
                 *reinterpret_cast<int2 *>(bo + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
@@ -712,8 +722,8 @@ template <int ALGO, bool RAG> __device__ __forceinline__ void siso_rows(const Si
     const int nw = (p.N + WIN - 1) / WIN;
     float4 *ck = p.ck + (long)wave * p.ck_stride;
     RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
-    siso<ALGO, WIN, RAG>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)nw * 4 * WAVE, lane,
-                         p.sf);
+    siso<ALGO, WIN, RAG>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)nw * 4 * WAVE, WAVE,
+                         lane, p.sf);
 }
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_siso_batch(SisoArgs p) {

@@ -122,22 +122,40 @@ int solve_circ(const int *Gp, int Z) {
 // Constellation table to device memory, in the arithmetic dtype.  The upload
 // synchronises once; later calls with the same table find it cached and stay
 // fully stream-ordered.
+// Device copy of a demapper table.  A table of M = 2^bps points (bps even,
+// >= 4) whose point m is exactly levI[m >> bps/2] + j levQ[m & (2^(bps/2)-1)]
+// is flagged separable and its axis levels are appended after the points.
 struct ConsCache {
     DevBuf buf;
     std::vector<double> host;
     bool f64 = false;
-    int upload(const void *cons, int cons_f64, int M, bool want_f64, hipStream_t st) {
+    int sep = 0, nbps = -1;
+    int upload(const void *cons, int cons_f64, int M, int bps, bool want_f64, hipStream_t st) {
         std::vector<double> d(2 * M);
         for (int i = 0; i < 2 * M; ++i)
             d[i] = cons_f64 ? ((const double *)cons)[i] : (double)((const float *)cons)[i];
-        if (buf.p && d == host && f64 == want_f64) return 0;
-        if (int rc = buf.ensure(sizeof(double) * 512)) return rc;
+        if (buf.p && d == host && f64 == want_f64 && nbps == bps) return 0;
+        if (int rc = buf.ensure(sizeof(double) * DM_TAB)) return rc;
+        int s = bps >= 4 && bps % 2 == 0 && M == (1 << bps);
+        const int K = bps / 2, L = 1 << K;
+        std::vector<double> lev;
+        if (s) {
+            lev.resize(2 * L);
+            for (int a = 0; a < L; ++a) lev[a] = d[2 * (a << K)];
+            for (int q = 0; q < L; ++q) lev[L + q] = d[2 * q + 1];
+            for (int m = 0; m < M && s; ++m)
+                s = d[2 * m] == lev[m >> K] && d[2 * m + 1] == lev[L + (m & (L - 1))];
+        }
+        if (s) d.insert(d.end(), lev.begin(), lev.end());
         std::vector<float> f(d.begin(), d.end());   // exact: an f32 table only meets f32 arithmetic
-        if (want_f64) HIPCHK(hipMemcpyAsync(buf.p, d.data(), sizeof(double) * 2 * M, hipMemcpyHostToDevice, st));
-        else HIPCHK(hipMemcpyAsync(buf.p, f.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice, st));
+        if (want_f64) HIPCHK(hipMemcpyAsync(buf.p, d.data(), sizeof(double) * d.size(), hipMemcpyHostToDevice, st));
+        else HIPCHK(hipMemcpyAsync(buf.p, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));
+        d.resize(2 * M);
         host = d;
         f64 = want_f64;
+        sep = s;
+        nbps = bps;
         return 0;
     }
 };
@@ -437,9 +455,9 @@ int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, cons
     ConsCache &cc = tbl[device & 15];
     const bool f64 = sym_f64 || cons_f64;
     hipStream_t st = (hipStream_t)stream;
-    if (int rc = cc.upload(cons, cons_f64, M, f64, st)) return rc;
+    if (int rc = cc.upload(cons, cons_f64, M, bps, f64, st)) return rc;
     DevBuf &tb = cc.buf;
-    DemapCfg c{M, div_f32, sign, (0.005 > noise_var) ? 0.005 : noise_var};
+    DemapCfg c{M, div_f32, sign, (0.005 > noise_var) ? 0.005 : noise_var, cc.sep};
     if (f64) {
         if (sym_f64) return launch_demap<double, double>(bps, (const double *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
         return launch_demap<double, float>(bps, (const float *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
@@ -480,8 +498,8 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = check_demap_args(M, bps)) return rc;
     Guard g(h->device);
     hipStream_t st = (hipStream_t)stream;
-    if (int rc = h->cons.upload(cons, cons_f64, M, cons_f64 != 0, st)) return rc;
-    DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var};
+    if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
+    DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep};
     const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
     const int chunks = (h->N + DM_KC - 1) / DM_KC;
     const dim3 grid((unsigned)((long)n_tiles_of(B) * chunks));

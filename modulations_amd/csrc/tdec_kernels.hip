@@ -788,7 +788,20 @@ template <typename T> __device__ __forceinline__ T cabs_np(T re, T im) {
 struct DemapCfg {
     int M, div_f32, sign;
     double nv;                 // max(noise_var, 0.005) already applied (:202)
+    int sep;                   // table is a separable square QAM grid: per-axis levels follow the points
 };
+constexpr int DM_TAB = 512 + 64;   // LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels)
+
+// One LLR from the two per-half minima (:219-225): NaN propagates, then the
+// division by the noise variance, the +-30 clip and the caller's sign.
+template <typename T> __device__ __forceinline__ double llr_of(T lo, T hi, const DemapCfg &c) {
+    const T diff = lo - hi;
+    double v;
+    if (sizeof(T) == 4 && c.div_f32) v = (double)((float)diff / (float)c.nv);
+    else v = (double)diff / c.nv;
+    if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);   // np.clip(llr, -30, 30)
+    return c.sign < 0 ? -v : v;
+}
 
 // All BPS LLRs of one symbol, reference sign (positive -> bit 1) unless
 // c.sign < 0.  Streams over the M points keeping a running min per bit and
@@ -821,27 +834,107 @@ __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapC
         }
     }
 #pragma unroll
-    for (int b = 0; b < BPS; ++b) {
-        const T lo = n0[b] ? (T)NAN : m0[b];   // np.min propagates NaN
-        const T hi = n1[b] ? (T)NAN : m1[b];
-        const T diff = lo - hi;
-        double v;
-        if (sizeof(T) == 4 && c.div_f32) v = (double)((float)diff / (float)c.nv);
-        else v = (double)diff / c.nv;
-        if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);   // np.clip(llr, -30, 30)
-        out[b] = c.sign < 0 ? -v : v;
+    for (int b = 0; b < BPS; ++b)
+        out[b] = llr_of<T>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
+}
+
+// Square QAM whose label splits into K I-bits and K Q-bits (16/64/256QAM of
+// sdr_modem.py:142-220): point (a, q) = levI[a] + j levQ[q].  The minimum of
+// numpy's |s - c|^2 over a bit-half is taken at the point nearest in plain
+// dx^2 + dy^2 (computed from the same rounded differences) unless two points of
+// the half are within a relative 64 ulp of each other: that point is found per
+// axis (2^K levels instead of 2^(2K) points) and only the 2*BPS candidates get
+// numpy's distance.  Near ties, non-finite input or underflow return false and
+// the caller runs the full scan, so the result is the scan's, bit for bit.
+template <typename T, int BPS>
+__device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    constexpr int K = BPS / 2, L = 1 << K;
+    const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
+    const T inf = (T)INFINITY;
+    const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
+    T best[2][K][2], second[2][K][2], all1[2], all2[2];
+    int arg[2][K][2], allarg[2];
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        const T s = ax ? si : sr;
+        const T *lev = ax ? lev_q : lev_i;
+        all1[ax] = all2[ax] = inf;
+        allarg[ax] = 0;
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                best[ax][b][v] = second[ax][b][v] = inf;
+                arg[ax][b][v] = 0;
+            }
+#pragma unroll
+        for (int a = 0; a < L; ++a) {
+            const T d = s - lev[a];
+            const T d2 = d * d;
+            all2[ax] = d2 < all1[ax] ? all1[ax] : (d2 < all2[ax] ? d2 : all2[ax]);
+            allarg[ax] = d2 < all1[ax] ? a : allarg[ax];
+            all1[ax] = d2 < all1[ax] ? d2 : all1[ax];
+#pragma unroll
+            for (int b = 0; b < K; ++b) {
+                const int v = (a >> (K - 1 - b)) & 1;
+                T &b1 = best[ax][b][v], &b2 = second[ax][b][v];
+                b2 = d2 < b1 ? b1 : (d2 < b2 ? d2 : b2);
+                arg[ax][b][v] = d2 < b1 ? a : arg[ax][b][v];
+                b1 = d2 < b1 ? d2 : b1;
+            }
+        }
     }
+    bool ok = all2[0] < inf && all2[1] < inf;   // every value finite (NaN compares false)
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax)
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const T e = best[ax][b][v] + all1[ax ^ 1];                  // the half's nearest point
+                const T tol = eps * e + tau;
+                ok = ok && second[ax][b][v] < inf && second[ax][b][v] - best[ax][b][v] > tol &&
+                     all2[ax ^ 1] - all1[ax ^ 1] > tol;
+            }
+    if (!ok) return false;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax)
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            T m[2];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int ia = ax ? allarg[0] : arg[0][b][v], iq = ax ? arg[1][b][v] : allarg[1];
+                const T a = cabs_np<T>(sr - lev_i[ia], si - lev_q[iq]);
+                m[v] = a * a;
+            }
+            out[ax * K + b] = llr_of<T>(m[0], m[1], c);
+        }
+    return true;
+}
+
+template <typename T, int BPS>
+__device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    if constexpr (BPS >= 4 && BPS % 2 == 0)
+        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return;
+    sym_llrs<T, BPS>(sr, si, cons, c, out);
+}
+
+// The table (and a separable table's axis levels) into LDS.
+template <typename T, int BPS> __device__ __forceinline__ void load_table(T *cons, const T *cons_g, const DemapCfg &c) {
+    const int n = 2 * c.M + (c.sep ? 2 * (1 << (BPS / 2)) : 0);
+    for (int i = threadIdx.x; i < n; i += BLOCK) cons[i] = cons_g[i];
 }
 
 template <typename T, typename S, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap(const S *syms, long n_sym, const T *cons_g, DemapCfg c, double *llr) {
-    __shared__ T cons[512];
-    for (int i = threadIdx.x; i < 2 * c.M; i += BLOCK) cons[i] = cons_g[i];
+    __shared__ T cons[DM_TAB];
+    load_table<T, BPS>(cons, cons_g, c);
     __syncthreads();
     const long s = (long)blockIdx.x * BLOCK + threadIdx.x;
     if (s >= n_sym) return;
     double v[BPS];
-    sym_llrs<T, BPS>((T)syms[2 * s], (T)syms[2 * s + 1], cons, c, v);
+    demap_sym<T, BPS>((T)syms[2 * s], (T)syms[2 * s + 1], cons, c, v);
 #pragma unroll
     for (int b = 0; b < BPS; ++b) llr[s * BPS + b] = v[b];
 }
@@ -865,9 +958,9 @@ template <typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *src, const int *off, long n_avail,
                                                        float *planes) {
-    __shared__ T cons[512];
+    __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
-    for (int i = threadIdx.x; i < 2 * c.M; i += BLOCK) cons[i] = cons_g[i];
+    load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + DM_KC - 1) / DM_KC;
     const long tile = blockIdx.x / chunks;
     const int k0 = (int)(blockIdx.x % chunks) * DM_KC;
@@ -883,7 +976,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         if (cw >= B || s >= S) continue;
         const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
         double v[BPS];
-        sym_llrs<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+        demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
 #pragma unroll
         for (int b = 0; b < BPS; ++b) {
             const long j = s * BPS + b;

@@ -223,6 +223,46 @@ def test_demap_high_order_vs_oracle(mod):
         assert np.array_equal(D.compute_llr(syms, mod, nv, sign=-1), -ref, equal_nan=True)
 
 
+def _adversarial_symbols(cons, rng, n):
+    """Symbols that stress the separable-QAM candidate search: exactly on points,
+    on decision bisectors (exact ties), within a few ulp of a bisector, far
+    outside the grid, tiny, huge, NaN/inf, plus noisy points."""
+    lv = np.unique(cons.real.astype(np.float64))
+    mids = (lv[:-1] + lv[1:]) / 2
+    pts = [cons[rng.integers(0, len(cons), n)] + 0.3 * (rng.standard_normal(n) + 1j * rng.standard_normal(n)),
+           cons[rng.integers(0, len(cons), 50)],
+           rng.choice(mids, 50) + 1j * rng.choice(lv, 50),
+           rng.choice(lv, 50) + 1j * rng.choice(mids, 50),
+           rng.choice(mids, 50) + 1j * rng.choice(mids, 50),
+           np.nextafter(rng.choice(mids, 50), 9) + 1j * np.nextafter(rng.choice(mids, 50), -9),
+           (rng.choice(mids, 50) + 1e-7) + 1j * rng.choice(lv, 50),
+           10 * (rng.standard_normal(50) + 1j * rng.standard_normal(50)),
+           1e-20 * (rng.standard_normal(20) + 1j * rng.standard_normal(20)),
+           np.array([0, 1e30, -1e30j, 3e38 + 3e38j, np.nan, np.inf, -np.inf + 1j, 1 + np.nan * 1j])]
+    return np.concatenate(pts)
+
+
+@pytest.mark.parametrize("mod", ["16QAM", "64QAM", "256QAM"])
+@pytest.mark.parametrize("dt", [np.complex64, np.complex128])
+def test_demap_separable_qam_adversarial(mod, dt):
+    """The per-axis candidate search (k_demap/k_demap_planes on square QAM) must
+    equal the full scan of compute_llr bit for bit, near-ties included."""
+    rng = np.random.default_rng(12)
+    cons = D.constellation(mod)
+    syms = _adversarial_symbols(cons, rng, 4000).astype(dt)
+    bps = D.MODULATIONS[mod]["bps"]
+    for nv in (np.float64(0.05), 0.01):
+        f64, div32, nve = D.demap_mode(syms.dtype, cons.dtype, nv)
+        ref = O.demap(syms, cons, bps, nve, div_f32=div32)
+        got = D.compute_llr(syms, mod, nv)
+        assert np.array_equal(got, ref, equal_nan=True)
+    # the device tensor path and the fused planes path share the device code
+    dev = D.compute_llr_device(torch.from_numpy(syms).cuda(), mod, np.float64(0.05))
+    torch.cuda.synchronize()
+    _, div32, nve = D.demap_mode(syms.dtype, cons.dtype, np.float64(0.05))
+    assert np.array_equal(dev.cpu().numpy(), O.demap(syms, cons, bps, nve, div_f32=div32), equal_nan=True)
+
+
 def test_demap_device_tensor():
     rng = np.random.default_rng(6)
     cons = D.constellation("16QAM")

@@ -1,4 +1,5 @@
-"""ctypes binding of the gfx950 HIP library (modulations_amd/lib/libtdec.so).
+"""ctypes bindings of the gfx950 HIP libraries (modulations_amd/lib/libtdec.so:
+turbo decoder + soft demapper; modulations_amd/lib/libmodem.so: modem front-end).
 
 The product path has no CPU fallback: if the library is missing or no HIP
 device is visible, calls raise instead of computing anything on the host.
@@ -115,3 +116,58 @@ def stream_ptr(stream):
     if stream is None:
         return None
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+# ---------------------------------------------------------------- libmodem.so ----------
+MODEM_LIB_PATH = os.path.join(HERE, "lib", "libmodem.so")
+MDM_ENAN = -8
+# every symbol include/modem.h declares
+MODEM_EXPORTS = (
+    "mdm_map_dev", "mdm_map", "mdm_demod_dev", "mdm_demod", "mdm_fir_dev", "mdm_fir",
+    "mdm_iq_quantize_dev", "mdm_iq_quantize", "mdm_iq_dequantize_dev", "mdm_iq_dequantize", "mdm_last_error",
+)
+_mlib = None
+
+
+def _declare_modem(L):
+    i, l, d = C.c_int, C.c_long, C.c_double
+    L.mdm_map_dev.argtypes = [i, _vp, l, i, _vp, i, _vp, _vp]
+    L.mdm_map.argtypes = [i, _vp, l, i, _vp, i, _vp]
+    L.mdm_demod_dev.argtypes = [i, i, _vp, i, l, i, _vp, d, _vp, i, _vp, _vp, _vp]
+    L.mdm_demod.argtypes = [i, i, _vp, i, l, i, _vp, d, _vp, i, _vp]
+    L.mdm_fir_dev.argtypes = [i, _vp, i, l, _vp, i, i, i, l, l, _vp, _vp]
+    L.mdm_fir.argtypes = [i, _vp, i, l, _vp, i, i, i, l, l, _vp]
+    L.mdm_iq_quantize_dev.argtypes = [i, _vp, i, l, _vp, _vp, _vp]
+    L.mdm_iq_quantize.argtypes = [i, _vp, i, l, _vp]
+    L.mdm_iq_dequantize_dev.argtypes = [i, _vp, l, _vp, _vp]
+    L.mdm_iq_dequantize.argtypes = [i, _vp, l, _vp]
+    for name in MODEM_EXPORTS:
+        getattr(L, name).restype = C.c_int
+    L.mdm_last_error.argtypes = []
+    L.mdm_last_error.restype = C.c_char_p
+
+
+def modem_lib():
+    """Load libmodem.so (building it first if this is a build tree without it)."""
+    global _mlib
+    if _mlib is None:
+        with _lock:
+            if _mlib is None:
+                if not os.path.exists(MODEM_LIB_PATH):
+                    from . import build
+                    build.build_modem()
+                L = C.CDLL(MODEM_LIB_PATH)
+                _declare_modem(L)
+                _mlib = L
+    return _mlib
+
+
+def modem_check(rc):
+    if rc == TDEC_OK:
+        return
+    msg = modem_lib().mdm_last_error().decode(errors="replace")
+    if rc in (TDEC_EINVAL, MDM_ENAN):
+        raise ValueError(msg)
+    if rc == TDEC_ENOMEM:
+        raise MemoryError(msg)
+    raise TdecError(f"modem error {rc}: {msg}")

@@ -1,4 +1,6 @@
-"""Build the gfx950 HIP library (modulations_amd/lib/libtdec.so) in-tree.
+"""Build the gfx950 HIP libraries in-tree: modulations_amd/lib/libtdec.so (turbo
+decoder + soft demapper, include/tdec.h) and modulations_amd/lib/libmodem.so
+(modem front-end, include/modem.h).
 
 ``python -m modulations_amd.build`` or ``modulations_amd.build.build()``.
 hipcc cross-compiles for gfx950 without a GPU.  Flags that the numerics need:
@@ -12,8 +14,13 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "tdec_api.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "tdec_kernels.hip"), os.path.join(ROOT, "include", "tdec.h")]
+DEPS = [SRC, os.path.join(HERE, "csrc", "tdec_kernels.hip"), os.path.join(HERE, "csrc", "npmath.hip"),
+        os.path.join(ROOT, "include", "tdec.h")]
 OUT = os.path.join(HERE, "lib", "libtdec.so")
+MODEM_SRC = os.path.join(HERE, "csrc", "modem_api.hip")
+MODEM_DEPS = [MODEM_SRC, os.path.join(HERE, "csrc", "modem_kernels.hip"), os.path.join(HERE, "csrc", "npmath.hip"),
+              os.path.join(ROOT, "include", "modem.h")]
+MODEM_OUT = os.path.join(HERE, "lib", "libmodem.so")
 
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-gpu-flush-denormals-to-zero", "-Wall", "-Wno-unused-value", "-Wno-unused-result"]
@@ -26,16 +33,26 @@ def hipcc():
     return "hipcc"
 
 
-def build(force=False, extra=()):
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
-        return OUT
-    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", OUT, SRC]
+def _build_one(src, deps, out, force, extra):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", out, src]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError("hipcc failed building libtdec.so")
-    return OUT
+        raise RuntimeError(f"hipcc failed building {os.path.basename(out)}")
+    return out
+
+
+def build(force=False, extra=()):
+    """Both libraries; returns the path of libtdec.so."""
+    _build_one(MODEM_SRC, MODEM_DEPS, MODEM_OUT, force, extra)
+    return _build_one(SRC, DEPS, OUT, force, extra)
+
+
+def build_modem(force=False):
+    return _build_one(MODEM_SRC, MODEM_DEPS, MODEM_OUT, force, ())
 
 
 def build_variant(name, defines):

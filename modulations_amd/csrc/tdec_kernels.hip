@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "npmath.hip"
+
 namespace tdec {
 
 constexpr int NS = 16;
@@ -766,24 +768,8 @@ __global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float 
 }
 
 // ---- soft demapper (compute_llr, test_sdr_with_coding.py:200-225) -----------------
-// numpy's complex |z| (SIMD loop of umath, FMA host): larger*sqrt(fma(r,r,1)).
-template <typename T> __device__ __forceinline__ T cabs_np(T re, T im) {
-    const T inf = (T)INFINITY;
-    re = fabs(re);
-    im = fabs(im);
-    const bool re_inf = re == inf, im_inf = im == inf;
-    im = re_inf ? inf : im;
-    re = im_inf ? inf : re;
-    const bool re_nn = re == re, im_nn = im == im;
-    im = re_nn ? im : (T)NAN;
-    re = im_nn ? re : (T)NAN;
-    const T larger = re > im ? re : im;
-    const T smaller = im < re ? im : re;
-    const bool div = !(larger == (T)0 || smaller == inf);
-    const T ratio = div ? smaller / larger : (T)0;
-    const T h = sqrt(fma(ratio, ratio, (T)1));
-    return h * larger;
-}
+// numpy's complex |z|: npmath.hip
+using npm::cabs_np;
 
 struct DemapCfg {
     int M, div_f32, sign;

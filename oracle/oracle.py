@@ -129,3 +129,98 @@ def demap(syms, constellation, bps, noise_var, div_f32=False):
     cons = np.ascontiguousarray(constellation.astype(np.complex64).view(np.float32))
     lib().orc_demap_c64(s, len(syms), cons, M, bps, float(noise_var), int(div_f32), out)
     return out
+
+
+# ---------------------------------------------------------------- modem oracle -------------
+# modem_oracle.c: the reference's mappers, hard demods, FIR forms and IQ
+# sample format.  Same rule: tests only.
+_MSO = os.path.join(_HERE, "liboracle_modem.so")
+_mlib = None
+_i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
+
+
+def mlib():
+    global _mlib
+    if _mlib is None:
+        if not os.path.exists(_MSO):
+            build()
+        L = C.CDLL(_MSO)
+        L.orm_map.argtypes = [_u8p, C.c_long, C.c_int, _f64p, _f64p]
+        L.orm_demod_gt0.argtypes = [_f64p, C.c_long, _u8p]
+        L.orm_demod_qpsk.argtypes = [_f64p, C.c_long, _u8p]
+        L.orm_demod_psk8_f32.argtypes = [_f32p, C.c_long, _i32p, C.c_int, _u8p]
+        L.orm_demod_psk8_f32.restype = C.c_long
+        L.orm_demod_psk8_f64.argtypes = [_f64p, C.c_long, _i32p, C.c_int, _u8p]
+        L.orm_demod_psk8_f64.restype = C.c_long
+        L.orm_demod_qam_axis.argtypes = [_f64p, C.c_long, C.c_int, C.c_double, _i32p, _u8p]
+        L.orm_demod_qam_axis.restype = C.c_long
+        L.orm_demod_argmin.argtypes = [_f64p, C.c_long, C.c_int, _f64p, _u8p]
+        L.orm_fir.argtypes = [_f64p, C.c_long, _f64p, C.c_int, C.c_int, C.c_int, C.c_long, C.c_long, _f64p]
+        L.orm_iq_quantize_f64.argtypes = [_f64p, C.c_long, _i8p]
+        L.orm_iq_quantize_f32.argtypes = [_f32p, C.c_long, _i8p]
+        L.orm_iq_dequantize.argtypes = [_u8p, C.c_long, _f32p]
+        _mlib = L
+    return _mlib
+
+
+def _c128(x):
+    return np.ascontiguousarray(np.asarray(x).astype(np.complex128).ravel()).view(np.float64)
+
+
+def modem_map(bits, bps, table):
+    bits = np.ascontiguousarray(np.asarray(bits).ravel(), np.uint8)
+    n_sym = -(-bits.size // bps)
+    out = np.zeros(2 * n_sym)
+    mlib().orm_map(bits, bits.size, bps, _c128(table), out)
+    return out.view(np.complex128).astype(np.asarray(table).dtype)
+
+
+def modem_demod(syms, kind, bps, labels=None, scale=0.0, cons=None, nan_raises=True):
+    """(bits uint8, nan count) of the rule `kind` (0 GT0, 1 QPSK, 2 PSK8, 3 QAM_AXIS, 4 ARGMIN)."""
+    syms = np.asarray(syms).ravel()
+    n = syms.size
+    out = np.zeros(n * bps, np.uint8)
+    L = mlib()
+    nans = 0
+    if kind == 0:
+        L.orm_demod_gt0(_c128(syms), n, out)
+    elif kind == 1:
+        L.orm_demod_qpsk(_c128(syms), n, out)
+    elif kind == 2:
+        lab = np.ascontiguousarray(np.arange(8) if labels is None else labels, np.int32)
+        if syms.dtype == np.complex64:
+            nans = L.orm_demod_psk8_f32(np.ascontiguousarray(syms).view(np.float32), n, lab, int(nan_raises), out)
+        else:
+            nans = L.orm_demod_psk8_f64(_c128(syms), n, lab, int(nan_raises), out)
+    elif kind == 3:
+        k = bps // 2
+        lab = np.ascontiguousarray(np.arange(1 << k) if labels is None else labels, np.int32)
+        nans = L.orm_demod_qam_axis(_c128(syms), n, k, float(scale), lab, out)
+    else:
+        L.orm_demod_argmin(_c128(syms), n, bps, _c128(cons), out)
+    return out, nans
+
+
+def modem_fir(x, taps, up, down, offset, n_out):
+    out = np.zeros(2 * n_out)
+    xs = _c128(x)
+    h = np.ascontiguousarray(taps, np.float64)
+    mlib().orm_fir(xs, xs.size // 2, h, h.size, up, down, offset, n_out, out)
+    return out.view(np.complex128)
+
+
+def modem_iq_quantize(sig):
+    sig = np.asarray(sig).ravel()
+    out = np.zeros(2 * sig.size, np.int8)
+    if sig.dtype == np.complex64:
+        mlib().orm_iq_quantize_f32(np.ascontiguousarray(sig).view(np.float32), sig.size, out)
+    else:
+        mlib().orm_iq_quantize_f64(_c128(sig), sig.size, out)
+    return out
+
+
+def modem_iq_dequantize(raw):
+    raw = np.ascontiguousarray(np.asarray(raw, np.uint8).ravel())
+    out = np.zeros(2 * (raw.size // 2), np.float32)
+    mlib().orm_iq_dequantize(raw, raw.size // 2, out)
+    return out.view(np.complex64)

@@ -83,7 +83,12 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
 // log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) with the
 // historic 37 cut-off.  The correction is defined as this exact sequence of f32
 // IEEE operations (explicit fused multiply-adds, no division), the same
-// sequence the oracle restates, so log-MAP is bit-exact too.
+// sequence the oracle restates, so log-MAP is bit-exact too.  In the
+// recursions each state's two parallel branches are combined first,
+// max*(m + g, m + g') = m + max*(g, g') (exact in real arithmetic), so an alpha
+// or beta step costs 8 shared pair max* + 16, not 48; the extrinsic keeps one
+// max* per branch.  Result: within 4e-6 of log-MAP with exact f64 Jacobian
+// logarithms (tests/test_oracle_golden.py).
 __device__ __forceinline__ float jac_corr(float d) {   // log1p(exp(-d)), 0 <= d <= 37
     const float x0 = d * 0x1.715476p+0f;                     /* d * log2(e) */
     const int n = (int)x0;
@@ -157,6 +162,15 @@ __device__ __forceinline__ void pair_max(const float (&g)[8], float (&pm)[2][4])
         pm[1][wy] = fmaxf(g[4 + wy], -g[4 + 3 - wy]);    // g(A0 B1 wy), g(A1 B0 wy) = -g(A0 B1 ~wy)
     }
 }
+// log-MAP's pair values: max*(g(input 0), g(input 3)) and max*(g(input 1), g(input 2))
+// (jac is symmetric except for NaN operands, so the order is part of the definition)
+__device__ __forceinline__ void pair_jac(const float (&g)[8], float (&pm)[2][4]) {
+#pragma unroll
+    for (int wy = 0; wy < 4; ++wy) {
+        pm[0][wy] = jac(g[wy], -g[3 - wy]);
+        pm[1][wy] = jac(g[4 + wy], -g[4 + 3 - wy]);
+    }
+}
 __device__ __forceinline__ float pm_of(const float (&pm)[2][4], int s, int inp) {
     return pm[t_dk(s, inp) ^ sb(s, 2) ^ sb(s, 3)][t_ow(s, inp) * 2 + t_oy(s, inp)];
 }
@@ -200,16 +214,16 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
         }
         return;
     }
+    // log-MAP: the parallel pair first, PM = max*(g(lower input), g(higher input)),
+    // then max* over the two predecessors in table order (p0, p0 + 8)
+    float pm[2][4];
+    pair_jac(g, pm);
     float na[NS];
 #pragma unroll
     for (int ns = 0; ns < NS; ++ns) {
-        float m = acc_first<ALGO>(a[t_prev_s(ns, 0)] + gam(g, t_prev_s(ns, 0), t_prev_i(ns, 0)));
-#pragma unroll
-        for (int idx = 1; idx < 4; ++idx) {
-            const int ps = t_prev_s(ns, idx), in = t_prev_i(ns, idx);
-            m = acc<ALGO>(m, a[ps] + gam(g, ps, in));
-        }
-        na[ns] = m;
+        const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
+        const float m = acc_first<ALGO>(a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)));
+        na[ns] = acc<ALGO>(m, a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
     }
     const float norm = na[0];
 #pragma unroll
@@ -237,13 +251,14 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
         }
         return;
     }
+    // log-MAP: pair class {0, 3} (successor next(s, 0)) first, then {1, 2}
+    float pm[2][4];
+    pair_jac(g, pm);
     float nb[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        float m = acc_first<ALGO>(b[t_next(s, 0)] + gam(g, s, 0));
-#pragma unroll
-        for (int inp = 1; inp < 4; ++inp) m = acc<ALGO>(m, b[t_next(s, inp)] + gam(g, s, inp));
-        nb[s] = m;
+        const float m = acc_first<ALGO>(b[t_next(s, 0)] + pm_of(pm, s, 0));
+        nb[s] = acc<ALGO>(m, b[t_next(s, 1)] + pm_of(pm, s, 1));
     }
     const float norm = nb[0];
 #pragma unroll

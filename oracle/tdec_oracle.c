@@ -183,10 +183,21 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
         for (int k = 0; k < N; ++k) {
             for (int n = 0; n < NS; ++n) {
                 float mv = (float)NEG_INF_VAL;
-                for (int idx = 0; idx < 4; ++idx) {
-                    int p = ps[n * 4 + idx], in = pi[n * 4 + idx];
-                    float t = ALP(k, p) + GAM(k, p, in);
-                    mv = algo ? jac(mv, t) : maxlog_acc(mv, t);
+                if (algo) {
+                    /* log-MAP (build-defined): each predecessor's two parallel
+                     * branches first, max*(gamma(lower input), gamma(higher input)),
+                     * then max* over the predecessors in table order */
+                    for (int idx = 0; idx < 4; idx += 2) {
+                        int p = ps[n * 4 + idx], i0 = pi[n * 4 + idx], i1 = pi[n * 4 + idx + 1];
+                        int lo = i0 < i1 ? i0 : i1, hi = i0 < i1 ? i1 : i0;
+                        mv = jac(mv, ALP(k, p) + jac(GAM(k, p, lo), GAM(k, p, hi)));
+                    }
+                } else {
+                    for (int idx = 0; idx < 4; ++idx) {
+                        int p = ps[n * 4 + idx], in = pi[n * 4 + idx];
+                        float t = ALP(k, p) + GAM(k, p, in);
+                        mv = maxlog_acc(mv, t);
+                    }
                 }
                 ALP(k + 1, n) = mv;
             }
@@ -202,10 +213,16 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
         for (int k = N - 1; k >= 0; --k) {
             for (int s = 0; s < NS; ++s) {
                 float mv = (float)NEG_INF_VAL;
-                for (int inp = 0; inp < 4; ++inp) {
-                    int n = nx[s * 4 + inp];
-                    float t = BET(k + 1, n) + GAM(k, s, inp);
-                    mv = algo ? jac(mv, t) : maxlog_acc(mv, t);
+                if (algo) {
+                    /* log-MAP: parallel pairs {0, 3} then {1, 2} (same successor each) */
+                    mv = jac(mv, BET(k + 1, nx[s * 4 + 0]) + jac(GAM(k, s, 0), GAM(k, s, 3)));
+                    mv = jac(mv, BET(k + 1, nx[s * 4 + 1]) + jac(GAM(k, s, 1), GAM(k, s, 2)));
+                } else {
+                    for (int inp = 0; inp < 4; ++inp) {
+                        int n = nx[s * 4 + inp];
+                        float t = BET(k + 1, n) + GAM(k, s, inp);
+                        mv = maxlog_acc(mv, t);
+                    }
                 }
                 BET(k, s) = mv;
             }

@@ -125,3 +125,47 @@ def test_logmap_max_star_accuracy():
     far = (a.astype(np.float64) - b) > 37
     assert np.all(np.abs(got - ref)[~far] <= 4e-6 * np.maximum(1, np.abs(ref[~far])))
     assert np.array_equal(got[far], a[far].astype(np.float64))
+
+
+def _logmap_f64_exact(Lc, La, sf, t):
+    """log-MAP with exact f64 Jacobian logarithms (np.logaddexp), the structure of
+    dvb_rcs2_turbo.py:116-281 with every max replaced: the accuracy anchor of the
+    build-defined f32 log-MAP (SURVEY §8 a11 / north star: within 1e-5)."""
+    nx, ow, oy, ps, pi = t
+    LcA, LcB, LcW, LcY = (x.astype(np.float64) for x in Lc)
+    N = len(LcA)
+    bA = np.array([0, 0, 1, 1]), np.array([0, 1, 0, 1])
+    iA, iB = LcA + La[0], LcB + La[1]
+    g = 0.5 * (iA[:, None, None] * (1 - 2 * bA[0])[None, None, :] + iB[:, None, None] * (1 - 2 * bA[1])[None, None, :]
+               + LcW[:, None, None] * (1 - 2 * ow)[None] + LcY[:, None, None] * (1 - 2 * oy)[None])
+    a = np.zeros((N + 1, 16))
+    for p in range(2):
+        if p:
+            a[0] = a[N]
+        for k in range(N):
+            a[k + 1] = np.logaddexp.reduce(a[k][ps] + g[k][ps, pi], axis=1)
+            a[k + 1] -= a[k + 1, 0]
+    b = np.zeros((N + 1, 16))
+    for p in range(2):
+        if p:
+            b[N] = b[0]
+        for k in range(N - 1, -1, -1):
+            b[k] = np.logaddexp.reduce(b[k + 1][nx] + g[k], axis=1)
+            b[k] -= b[k, 0]
+    app = np.logaddexp.reduce(a[:N, :, None] + g + b[1:][:, nx], axis=1)     # [N, 4]
+    LpA = np.logaddexp(app[:, 0], app[:, 1]) - np.logaddexp(app[:, 2], app[:, 3])
+    LpB = np.logaddexp(app[:, 0], app[:, 2]) - np.logaddexp(app[:, 1], app[:, 3])
+    return np.clip((LpA - iA) * sf, -300, 300), np.clip((LpB - iB) * sf, -300, 300)
+
+
+def test_logmap_siso_within_1e5_of_exact_log_map():
+    """The f32 log-MAP SISO (oracle == kernel bit for bit) stays within 1e-5 of
+    log-MAP computed with exact f64 Jacobian logarithms."""
+    rng = np.random.default_rng(1)
+    t, _ = O.trellis()
+    for trial, (sc, lsc, n) in enumerate(((1, 3, 48), (4, 3, 48), (2, 8, 212))):
+        Lc = (rng.standard_normal((4, n)) * sc).astype(np.float32)
+        La = rng.standard_normal((2, n)) * lsc
+        A, B = O.siso(*Lc, *La, t, 0.7, algo=1)
+        RA, RB = _logmap_f64_exact(Lc, La, 0.7, t)
+        assert max(np.max(np.abs(A - RA)), np.max(np.abs(B - RB))) < 1e-5, trial

@@ -6,6 +6,7 @@
 // stream and synchronise.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -108,12 +109,12 @@ int mdm_map_dev(int device, const uint8_t *d_bits, long n_bits, int bps, const v
     std::memcpy(table_f64 ? (void *)t.d : (void *)t.f, table, (size_t)(2 << bps) * (table_f64 ? 8 : 4));
     const long n_sym = (n_bits + bps - 1) / bps;
     hipStream_t st = (hipStream_t)stream;
+    long nblk = (n_sym + MAP_SPB - 1) / MAP_SPB;
+    const dim3 grid((unsigned)(nblk < 256L * 8 ? nblk : 256L * 8));
     if (table_f64)
-        hipLaunchKernelGGL((k_map<double>), grid_for(n_sym), dim3(BLOCK), 0, st, d_bits, n_bits, bps, n_sym, t,
-                           (double2 *)d_syms);
+        hipLaunchKernelGGL((k_map<double>), grid, dim3(BLOCK), 0, st, d_bits, n_bits, bps, n_sym, t, (double2 *)d_syms);
     else
-        hipLaunchKernelGGL((k_map<float>), grid_for(n_sym), dim3(BLOCK), 0, st, d_bits, n_bits, bps, n_sym, t,
-                           (float2 *)d_syms);
+        hipLaunchKernelGGL((k_map<float>), grid, dim3(BLOCK), 0, st, d_bits, n_bits, bps, n_sym, t, (float2 *)d_syms);
     return launch_check("k_map");
 }
 
@@ -178,6 +179,7 @@ int mdm_demod_dev(int device, int kind, const void *d_syms, int sym_f64, long n_
     if (int rc = demod_args(kind, bps, labels, scale, cons, nan_raises, a)) return rc;
     if (n_sym == 0) return 0;
     if (!d_syms || !d_bits) return fail(MDM_EINVAL, "null buffer");
+    a.vec = ((uintptr_t)d_bits % bps) == 0;
     Guard g(device);
     hipStream_t st = (hipStream_t)stream;
     if (sym_f64)
@@ -224,6 +226,8 @@ static int fir_plan(long n_x, int n_taps, int up, int down, long offset, long n_
     a.off = offset;
     a.n_out = n_out;
     a.n_x = n_x;
+    if ((n_out - 1) * down + offset + n_taps >= (1L << 31) || n_x * (long)up + n_taps >= (1L << 31))
+        return fail(MDM_EINVAL, "FIR too long for one call (2^31 samples)");
     a.per_thread = down == 1 ? 4 : 1;
     const long opb = (long)BLOCK * a.per_thread;
     const long span = ((opb - 1) * down + n_taps - 1) / up + 2;   // staged samples per block (upper bound)
@@ -248,6 +252,30 @@ int mdm_fir_dev(int device, const void *d_x, int x_f64, long n_x, const double *
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)blocks);
     double2 *o = (double2 *)d_out;
+    // polyphase up-sampler / phase-major decimator for the shapes the reference uses
+    if (down == 1 && (up == 2 || up == 4 || up == 8 || up == 16)) {
+        const long nper = (n_out - 1 + offset) / up + 1;
+        const dim3 g2((unsigned)std::min<long>((nper + BLOCK - 1) / BLOCK, 256L * 16));
+#define UPC(U)                                                                                                  \
+    case U:                                                                                                     \
+        if (x_f64) hipLaunchKernelGGL((k_fir_up<double, U>), g2, dim3(BLOCK), 0, st, (const double2 *)d_x, a, o); \
+        else hipLaunchKernelGGL((k_fir_up<float, U>), g2, dim3(BLOCK), 0, st, (const float2 *)d_x, a, o);         \
+        break;
+        switch (up) { UPC(2) UPC(4) UPC(8) UPC(16) }
+#undef UPC
+        return launch_check("k_fir_up");
+    }
+    if (up == 1 && (down == 1 || down == 2 || down == 4 || down == 8)) {
+        const dim3 g2((unsigned)std::min<long>((n_out + BLOCK - 1) / BLOCK, 256L * 16));
+#define DNC(D)                                                                                                    \
+    case D:                                                                                                       \
+        if (x_f64) hipLaunchKernelGGL((k_fir_dec<double, D>), g2, dim3(BLOCK), 0, st, (const double2 *)d_x, a, o); \
+        else hipLaunchKernelGGL((k_fir_dec<float, D>), g2, dim3(BLOCK), 0, st, (const float2 *)d_x, a, o);         \
+        break;
+        switch (down) { DNC(1) DNC(2) DNC(4) DNC(8) }
+#undef DNC
+        return launch_check("k_fir_dec");
+    }
     if (x_f64 && stage) hipLaunchKernelGGL((k_fir<double, true>), grid, dim3(BLOCK), 0, st, (const double2 *)d_x, a, o);
     else if (x_f64) hipLaunchKernelGGL((k_fir<double, false>), grid, dim3(BLOCK), 0, st, (const double2 *)d_x, a, o);
     else if (stage) hipLaunchKernelGGL((k_fir<float, true>), grid, dim3(BLOCK), 0, st, (const float2 *)d_x, a, o);
@@ -316,8 +344,9 @@ int mdm_iq_dequantize_dev(int device, const uint8_t *d_raw, long n_pairs, float 
     if (n_pairs == 0) return 0;
     if (!d_raw || !d_sig) return fail(MDM_EINVAL, "null buffer");
     Guard g(device);
-    hipLaunchKernelGGL(k_dequantize, grid_for(n_pairs), dim3(BLOCK), 0, (hipStream_t)stream, (const uchar2 *)d_raw,
-                       n_pairs, (float2 *)d_sig);
+    const int vec = ((uintptr_t)d_raw & 15) == 0 && ((uintptr_t)d_sig & 15) == 0;
+    hipLaunchKernelGGL(k_dequantize, grid_for(vec ? (n_pairs + 7) / 8 : n_pairs), dim3(BLOCK), 0, (hipStream_t)stream,
+                       d_raw, n_pairs, (float2 *)d_sig, vec);
     return launch_check("k_dequantize");
 }
 

@@ -36,11 +36,18 @@ template <typename T> struct C2;
 template <> struct C2<float> { typedef float2 t; };
 template <> struct C2<double> { typedef double2 t; };
 
+// One block-iteration maps MAP_SPB symbols: their label bytes (MAP_SPB * bps
+// <= 8 KiB) are staged in LDS with 16-B loads, then every thread reads its
+// symbols' bits from LDS and the stores run coalesced (consecutive threads,
+// consecutive symbols).
+constexpr int MAP_SPB = 1024;
+
 template <typename T>
 __global__ __launch_bounds__(BLOCK) void k_map(const uint8_t *__restrict__ bits, long n_bits, int bps, long n_sym,
                                                MapTable tab, typename C2<T>::t *__restrict__ out) {
     typedef typename C2<T>::t V;
     __shared__ V t[MAP_MAX];
+    __shared__ uint4 lb[MAP_SPB * 8 / 16];
     const T *src = sizeof(T) == 4 ? (const T *)tab.f : (const T *)tab.d;
     for (int i = threadIdx.x; i < (1 << bps); i += BLOCK) {
         V v;
@@ -48,22 +55,31 @@ __global__ __launch_bounds__(BLOCK) void k_map(const uint8_t *__restrict__ bits,
         v.y = src[2 * i + 1];
         t[i] = v;
     }
-    __syncthreads();
-    for (long s = gtid(); s < n_sym; s += gstride()) {
-        const long b0 = s * bps;
-        int lab = 0;
-        if (b0 + bps <= n_bits) {
-            for (int j = 0; j < bps; ++j) lab = (lab << 1) | (bits[b0 + j] & 1);
+    const uint8_t *lbytes = reinterpret_cast<const uint8_t *>(lb);
+    for (long s0 = (long)blockIdx.x * MAP_SPB; s0 < n_sym; s0 += (long)gridDim.x * MAP_SPB) {
+        const long b0 = s0 * bps;                       // first label byte of the block
+        const long nb = min((long)MAP_SPB * bps, n_bits - b0);
+        __syncthreads();
+        if (((uintptr_t)(bits + b0) & 15) == 0 && nb == (long)MAP_SPB * bps) {
+            const uint4 *g = reinterpret_cast<const uint4 *>(bits + b0);
+            for (int i = threadIdx.x; i < MAP_SPB * bps / 16; i += BLOCK) lb[i] = g[i];
         } else {
-            for (int j = 0; j < bps; ++j) lab = (lab << 1) | (b0 + j < n_bits ? (bits[b0 + j] & 1) : 0);
+            uint8_t *l = reinterpret_cast<uint8_t *>(lb);
+            for (int i = threadIdx.x; i < MAP_SPB * bps; i += BLOCK) l[i] = i < nb ? bits[b0 + i] : 0;
         }
-        out[s] = t[lab];
+        __syncthreads();
+        const int ns = (int)min((long)MAP_SPB, n_sym - s0);
+        for (int j = threadIdx.x; j < ns; j += BLOCK) {
+            int lab = 0;
+            for (int q = 0; q < bps; ++q) lab = (lab << 1) | (lbytes[j * bps + q] & 1);
+            out[s0 + j] = t[lab];
+        }
     }
 }
 
 // ---- hard demodulators -------------------------------------------------------------------
 struct DemodArgs {
-    int kind, bps, nan_raises, levels;
+    int kind, bps, nan_raises, levels, vec;   // vec: the output rows are aligned for one store per symbol
     double scale;
     int32_t labels[256];
     double cons[2 * ARG_MAX];
@@ -90,7 +106,8 @@ __global__ __launch_bounds__(BLOCK) void k_demod(const typename C2<T>::t *__rest
     uint32_t nans = 0;
     for (long s = gtid(); s < n_sym; s += gstride()) {
         const T re = syms[s].x, im = syms[s].y;
-        uint8_t *o = bits + s * a.bps;
+        uint8_t ob[8];
+        uint8_t *o = ob;
         if (a.kind == 0) {                      // MDM_DEMOD_GT0
             o[0] = re > (T)0;
         } else if (a.kind == 1) {               // MDM_DEMOD_QPSK
@@ -135,6 +152,18 @@ __global__ __launch_bounds__(BLOCK) void k_demod(const typename C2<T>::t *__rest
             }
             for (int b = 0; b < a.bps; ++b) o[b] = (idx >> (a.bps - 1 - b)) & 1;
         }
+        // one store per symbol where the width allows (the rows stay coalesced)
+        uint8_t *dst = bits + s * a.bps;
+        if (a.vec && a.bps == 8) {
+            *reinterpret_cast<uint2 *>(dst) = make_uint2(ob[0] | ob[1] << 8 | ob[2] << 16 | (unsigned)ob[3] << 24,
+                                                         ob[4] | ob[5] << 8 | ob[6] << 16 | (unsigned)ob[7] << 24);
+        } else if (a.vec && a.bps == 4) {
+            *reinterpret_cast<unsigned *>(dst) = ob[0] | ob[1] << 8 | ob[2] << 16 | (unsigned)ob[3] << 24;
+        } else if (a.vec && a.bps == 2) {
+            *reinterpret_cast<unsigned short *>(dst) = (unsigned short)(ob[0] | ob[1] << 8);
+        } else {
+            for (int b = 0; b < a.bps; ++b) dst[b] = ob[b];
+        }
     }
     if (nan_count && nans) atomicAdd(nan_count, nans);
 }
@@ -150,42 +179,44 @@ struct FirArgs {
 };
 constexpr int FIR_LDS = 3840;   // staged input samples (60 KiB of double2)
 
-__device__ __forceinline__ long fdiv_floor(long a, long b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int fdiv_floor(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
+// Index arithmetic is 32-bit (the host bounds n_out*down + off and n_x*up);
+// per output one division by `up` finds the first tap and its input sample,
+// then the tap loop steps k += up, m -= 1.
 template <typename T, bool STAGE>
 __global__ __launch_bounds__(BLOCK) void k_fir(const typename C2<T>::t *__restrict__ x, FirArgs a,
                                                double2 *__restrict__ out) {
     __shared__ double h[TAPS_MAX];
     __shared__ double2 xs[STAGE ? FIR_LDS : 1];
     for (int i = threadIdx.x; i < a.n_taps; i += BLOCK) h[i] = a.h[i];
-    const long opb = (long)BLOCK * a.per_thread;
-    const long i0 = (long)blockIdx.x * opb;
+    const int up = a.up, down = a.down, L = a.n_taps, nx = (int)a.n_x, off = (int)a.off;
+    const int opb = BLOCK * a.per_thread;
+    const int i0 = (int)blockIdx.x * opb;
     // input samples of this block's outputs: m in [m_lo, m_hi]
-    const long j_lo = i0 * a.down + a.off - (a.n_taps - 1);
-    const long j_hi = (i0 + opb - 1) * a.down + a.off;
-    long m_lo = -fdiv_floor(-j_lo, a.up);   // ceil(j_lo / up)
-    long m_hi = fdiv_floor(j_hi, a.up);
+    int m_lo = -fdiv_floor(-(i0 * down + off - (L - 1)), up);   // ceil(j_lo / up)
+    int m_hi = fdiv_floor((i0 + opb - 1) * down + off, up);
     m_lo = m_lo < 0 ? 0 : m_lo;
-    m_hi = m_hi > a.n_x - 1 ? a.n_x - 1 : m_hi;
+    m_hi = m_hi > nx - 1 ? nx - 1 : m_hi;
     if (STAGE) {
-        for (long m = m_lo + threadIdx.x; m <= m_hi; m += BLOCK) {
+        for (int m = m_lo + threadIdx.x; m <= m_hi; m += BLOCK) {
             const typename C2<T>::t v = x[m];
             xs[m - m_lo] = make_double2((double)v.x, (double)v.y);
         }
     }
     __syncthreads();
     for (int r = 0; r < a.per_thread; ++r) {
-        const long i = i0 + (long)r * BLOCK + threadIdx.x;
-        if (i >= a.n_out) break;
-        const long j0 = i * a.down + a.off;
-        // taps k with (j0 - k) % up == 0 and 0 <= (j0 - k) / up < n_x
-        long kmin = j0 - (a.n_x - 1) * a.up;
-        kmin = kmin < 0 ? 0 : kmin;
-        const long kmax = j0 < a.n_taps - 1 ? j0 : a.n_taps - 1;
-        long k = kmin + ((j0 - kmin) % a.up);
+        const int i = i0 + r * BLOCK + threadIdx.x;
+        if (i >= (int)a.n_out) break;
+        const int j0 = i * down + off;
+        // first tap k >= max(0, j0 - (nx-1)*up) with k == j0 (mod up); its sample m = (j0 - k) / up
+        const int mq = j0 / up, k_first = j0 - mq * up;           // largest m = mq (k = j0 mod up)
+        int m = mq < nx - 1 ? mq : nx - 1;
+        int k = j0 - m * up;
+        if (k < k_first) k = k_first;
+        const int kmax = j0 < L - 1 ? j0 : L - 1;
         double re = 0.0, im = 0.0;
-        for (; k <= kmax; k += a.up) {
-            const long m = (j0 - k) / a.up;
+        for (; k <= kmax; k += up, --m) {
             double xr, xi;
             if (STAGE) {
                 const double2 v = xs[m - m_lo];
@@ -203,20 +234,128 @@ __global__ __launch_bounds__(BLOCK) void k_fir(const typename C2<T>::t *__restri
     }
 }
 
+// Up-sampling form (down == 1), polyphase: thread = one input period m, i.e.
+// the UP outputs j = m*UP + p, p < UP, which all read x[m], x[m-1], ... : each
+// input sample is read from LDS once per period (not once per output) and the
+// taps h[p + r*UP] are wave-uniform (LDS broadcast).  Per output the terms are
+// summed in ascending k, exactly as k_fir does, so both forms agree bit for bit.
+template <typename T, int UP>
+__global__ __launch_bounds__(BLOCK) void k_fir_up(const typename C2<T>::t *__restrict__ x, FirArgs a,
+                                                  double2 *__restrict__ out) {
+    __shared__ double h[TAPS_MAX];
+    __shared__ double2 xs[BLOCK + TAPS_MAX];
+    for (int i = threadIdx.x; i < a.n_taps; i += BLOCK) h[i] = a.h[i];
+    const int L = a.n_taps, nx = (int)a.n_x, off = (int)a.off, n_out = (int)a.n_out;
+    const int R = (L + UP - 1) / UP;                 // input samples per period
+    const int nper = (n_out - 1 + off) / UP + 1;     // periods holding outputs
+    for (int m0 = (int)blockIdx.x * BLOCK; m0 < nper; m0 += (int)gridDim.x * BLOCK) {
+        __syncthreads();
+        const int lo = m0 - (R - 1);                 // xs[q] = x[lo + q], zero outside [0, nx)
+        for (int q = threadIdx.x; q < BLOCK + R - 1; q += BLOCK) {
+            const int mm = lo + q;
+            if (mm >= 0 && mm < nx) {
+                const typename C2<T>::t v = x[mm];
+                xs[q] = make_double2((double)v.x, (double)v.y);
+            } else {
+                xs[q] = make_double2(0.0, 0.0);
+            }
+        }
+        __syncthreads();
+        const int m = m0 + threadIdx.x;
+        if (m >= nper) continue;
+        double re[UP], im[UP];
+#pragma unroll
+        for (int p = 0; p < UP; ++p) re[p] = im[p] = 0.0;
+        for (int r = 0; r < R; ++r) {
+            const int mm = m - r;
+            if (mm < 0 || mm >= nx) continue;            // the term is absent (not a zero term)
+            const double2 v = xs[threadIdx.x + R - 1 - r];
+#pragma unroll
+            for (int p = 0; p < UP; ++p) {
+                const int k = p + r * UP;
+                if (k < L) {
+                    const double hk = a.h[k];   // wave-uniform: scalar load from the kernel arguments
+                    re[p] = fma(hk, v.x, re[p]);
+                    im[p] = fma(hk, v.y, im[p]);
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < UP; ++p) {
+            const int i = m * UP + p - off;
+            if (i >= 0 && i < n_out) out[i] = make_double2(re[p], im[p]);
+        }
+    }
+}
+
+// Decimating form (up == 1): thread = one output; the staged window is stored
+// phase-major (sample q at [q % DOWN][q / DOWN]) so the wave's reads of
+// x[i*DOWN + off - k] at one tap hit consecutive LDS words (no bank conflicts).
+template <typename T, int DOWN>
+__global__ __launch_bounds__(BLOCK) void k_fir_dec(const typename C2<T>::t *__restrict__ x, FirArgs a,
+                                                   double2 *__restrict__ out) {
+    constexpr int PL = (BLOCK * DOWN + TAPS_MAX + DOWN - 1) / DOWN + 1;   // samples per phase plane
+    __shared__ double h[TAPS_MAX];
+    __shared__ double2 xs[DOWN * PL];
+    for (int i = threadIdx.x; i < a.n_taps; i += BLOCK) h[i] = a.h[i];
+    const int L = a.n_taps, nx = (int)a.n_x, off = (int)a.off, n_out = (int)a.n_out;
+    for (int i0 = (int)blockIdx.x * BLOCK; i0 < n_out; i0 += (int)gridDim.x * BLOCK) {
+        __syncthreads();
+        const int lo = i0 * DOWN + off - (L - 1);     // first sample the block reads
+        const int span = (BLOCK - 1) * DOWN + L;
+        for (int q = threadIdx.x; q < span; q += BLOCK) {
+            const int mm = lo + q;
+            double2 v = make_double2(0.0, 0.0);
+            if (mm >= 0 && mm < nx) {
+                const typename C2<T>::t w = x[mm];
+                v = make_double2((double)w.x, (double)w.y);
+            }
+            xs[(q % DOWN) * PL + q / DOWN] = v;
+        }
+        __syncthreads();
+        const int i = i0 + threadIdx.x;
+        if (i >= n_out) continue;
+        const int j0 = i * DOWN + off;
+        double re = 0.0, im = 0.0;
+        // k in ascending order over the taps whose sample lies in [0, nx)
+        const int kmin = j0 - (nx - 1) > 0 ? j0 - (nx - 1) : 0;
+        const int kmax = j0 < L - 1 ? j0 : L - 1;
+        for (int k = kmin; k <= kmax; ++k) {
+            const int q = j0 - k - lo;                    // = threadIdx.x*DOWN + (L-1-k)
+            const double2 v = xs[(q % DOWN) * PL + q / DOWN];
+            re = fma(h[k], v.x, re);
+            im = fma(h[k], v.y, im);
+        }
+        out[i] = make_double2(re, im);
+    }
+}
+
 // ---- IQ sample conversion ------------------------------------------------------------------
 // max|sig| (np.max(np.abs(sig)), NaN propagating) as the largest bit pattern:
 // abs values are >= +0, so their IEEE bits order like unsigned integers and a
 // NaN outranks +inf.
+// numpy's |z| (a division and a square root) is evaluated only for samples
+// that can still be the maximum: a sample whose re^2 + im^2 (f64, < 1e-15
+// relative error) is below (1 - margin) x that of the largest sample seen by
+// this thread has a smaller numpy |z| than that sample (numpy's |z| is within
+// a few ulp of the true modulus: margin 1e-9 for complex128, 1e-5 for
+// complex64), so skipping it cannot change the maximum.
 template <typename T>
 __global__ __launch_bounds__(BLOCK) void k_absmax(const typename C2<T>::t *__restrict__ sig, long n,
                                                   unsigned long long *__restrict__ mx) {
     unsigned long long m = 0;
+    double thr = -1.0;   // (1 - 1e-9) * largest re^2 + im^2 seen so far
     for (long i = gtid(); i < n; i += gstride()) {
+        const double re = (double)sig[i].x, im = (double)sig[i].y;
+        const double q = fma(re, re, im * im);
+        if (q < thr) continue;                          // NaN q fails the test and is evaluated
         const T a = npm::cabs_np<T>(sig[i].x, sig[i].y);
         unsigned long long b;
         if (sizeof(T) == 8) b = (unsigned long long)__double_as_longlong((double)a);
         else b = (unsigned long long)(unsigned)__float_as_uint((float)a);
         m = b > m ? b : m;
+        const double t = q * (sizeof(T) == 8 ? 1.0 - 1e-9 : 1.0 - 1e-5);
+        thr = t > thr ? t : thr;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -249,12 +388,26 @@ __global__ __launch_bounds__(BLOCK) void k_quantize(const typename C2<T>::t *__r
     }
 }
 
-// (raw.astype(np.float32) - 127.5) / 127.5, I from even bytes, Q from odd
-__global__ __launch_bounds__(BLOCK) void k_dequantize(const uchar2 *__restrict__ raw, long n, float2 *__restrict__ sig) {
-    for (long i = gtid(); i < n; i += gstride()) {
-        const uchar2 r = raw[i];
-        sig[i] = make_float2(((float)r.x - 127.5f) / 127.5f, ((float)r.y - 127.5f) / 127.5f);
+// (raw.astype(np.float32) - 127.5) / 127.5, I from even bytes, Q from odd.
+// 8 samples (16 B in, 64 B out) per thread and step when both buffers are
+// 16-B aligned; the remaining samples one by one.
+__device__ __forceinline__ float deq(unsigned b) { return ((float)b - 127.5f) / 127.5f; }
+
+__global__ __launch_bounds__(BLOCK) void k_dequantize(const uint8_t *__restrict__ raw, long n, float2 *__restrict__ sig,
+                                                      int vec) {
+    const long n8 = vec ? n / 8 : 0;   // vec: both buffers 16-B aligned
+    const uint4 *r16 = reinterpret_cast<const uint4 *>(raw);
+    float4 *o16 = reinterpret_cast<float4 *>(sig);
+    for (long i = gtid(); i < n8; i += gstride()) {
+        const uint4 r = r16[i];
+        const unsigned w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            o16[4 * i + q] = make_float4(deq(w[q] & 255), deq((w[q] >> 8) & 255), deq((w[q] >> 16) & 255),
+                                         deq(w[q] >> 24));
     }
+    for (long i = 8 * n8 + gtid(); i < n; i += gstride())
+        sig[i] = make_float2(deq(raw[2 * i]), deq(raw[2 * i + 1]));
 }
 
 }  // namespace mdm

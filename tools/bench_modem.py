@@ -40,7 +40,7 @@ def timed(fn, reps, stream):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--msym", type=float, default=32, help="millions of symbols")
+    ap.add_argument("--msym", type=float, default=128, help="millions of symbols")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda:0")

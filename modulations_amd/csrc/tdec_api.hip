@@ -284,7 +284,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     int blocks_per_cu = 0, n_cu = 0;
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks_per_cu, decode_kernel(algo, n_couples % WIN != 0), BLOCK, 0);
+            &blocks_per_cu, decode_kernel(algo, n_couples % win_of(algo) != 0), BLOCK, 0);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
         tdec_destroy(h);
@@ -375,7 +375,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p, d_bits, d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % WIN != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
                        a, pm, iv);
     HIPCHK(hipGetLastError());
     return 0;
@@ -433,7 +433,7 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
     SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p, ck_stride_of(h)};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    const bool rag = h->N % WIN != 0;
+    const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
     if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
     else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
     else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);

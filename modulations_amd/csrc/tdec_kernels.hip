@@ -351,6 +351,30 @@ struct Raw {
     double2 l;
 };
 
+// ---- LDS-DMA staging (siso8) ----------------------------------------------------------
+// global_load_lds: the load writes LDS directly, lane l's bytes at base + l*size,
+// with no VGPR destination.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+__device__ __forceinline__ void glds16(const void *g, void *l) {
+    __builtin_amdgcn_global_load_lds((glb_void *)g, (lds_void *)l, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void *g, void *l) {
+    __builtin_amdgcn_global_load_lds((glb_void *)g, (lds_void *)l, 4, 0, 0);
+}
+// s_waitcnt vmcnt(8) (lgkmcnt / expcnt left open).  Vector-memory operations
+// retire in issue order, and at least 8 are issued after a window's LDS-DMA
+// (the 4 extrinsic stores of the bottom half and the 4 checkpoint loads of the
+// next window), so this retires the DMA without waiting for those stores.
+__device__ __forceinline__ void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70 | 8); }
+
+// A wave's staged half window: 4 steps x {16-B plane v, 16-B plane l} x 64 lanes.
+struct LdsStage {
+    float4 *v;
+    double2 *l;
+    int lane;
+};
+
 // Decoder 1 in the tile layout: X = [N][64] float4 {A, B, W1, Y1} (uniform
 // base), a-priori La = Le2[inv_perm[k]] ([N][64] double2, the same index for
 // every lane), or null for the all-zero a-priori of the first iteration
@@ -369,6 +393,16 @@ struct TileIn {
     }
     __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
         make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    }
+    __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
+        glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
+        if (La) glds16(&at(La, la_idx[k] * rs + lane), st.l + j * WAVE);
+    }
+    __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
+        Raw r;
+        r.v = st.v[j * WAVE + lane];
+        r.l = La ? st.l[j * WAVE + lane] : make_double2(0.0, 0.0);
+        return r;
     }
 };
 
@@ -392,6 +426,21 @@ struct TileInPre {
         iA = r.l.x;
         iB = r.l.y;
         gamma_from_sums(iA, iB, r.v.z, r.v.w, g);
+    }
+    // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
+    __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
+        const float *z = reinterpret_cast<const float *>(&at(Z, k * WAVE + lane));
+        float *dst = reinterpret_cast<float *>(st.v + j * WAVE);
+        glds4(z, dst);
+        glds4(z + 1, dst + WAVE);
+        glds16(&at(P, p_idx[k] * rs + lane), st.l + j * WAVE);
+    }
+    __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
+        const float *zp = reinterpret_cast<const float *>(st.v + j * WAVE);
+        Raw r;
+        r.v = make_float4(0.0f, 0.0f, zp[lane], zp[WAVE + lane]);
+        r.l = st.l[j * WAVE + lane];
+        return r;
     }
 };
 
@@ -638,13 +687,211 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     }
 }
 
+// ---- max-log SISO with alpha checkpoints every 8 steps ---------------------------
+// Halves the checkpoint stream of siso<> (16 B per step -> 8 B written, and the
+// same read back) at the cost of half an extra alpha step per position.  A
+// backward window of 8 positions is processed as two halves of 4: the top half
+// needs alpha[k0+4], i.e. 4 steps from the checkpoint over the BOTTOM half's
+// inputs, which are needed again for the bottom half itself.  Those inputs are
+// staged per lane in LDS (8 KiB per wave) by LDS-DMA (global_load_lds) issued
+// one window ahead, so they cost no VGPRs.  Every value is computed by the same f32/f64 operations in
+// the same order as siso<>, so the result is bit-identical.
+
+// Positions kb+3 .. kb of a half window (kb+len-1 .. kb if ragged), alpha[kb]
+// given, midpoint recompute as back_window.
+template <int ALGO, bool RAG, class Out>
+__device__ __forceinline__ void window_half(const Out &out, int kb, int len, const float (&a0)[NS],
+                                            const float (&gw)[4][8], const double (&iAw)[4], const double (&iBw)[4],
+                                            const float (&lcA)[4], const float (&lcB)[4], float (&b)[NS], double sf) {
+    constexpr int H = 2;
+    float am[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) am[s] = a0[s];
+#pragma unroll
+    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+        if (RAG && j >= len) continue;       // wave-uniform
+        __builtin_amdgcn_sched_barrier(0);
+        const int from = j >= H ? H : 0;
+        float aj[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            aj[s] = j >= H ? am[s] : a0[s];
+            asm volatile("" : "+v"(aj[s]));
+        }
+#pragma unroll
+        for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
+        double leA, leB;
+        extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
+        out.store(kb + j, leA, leB, lcA[j], lcB[j]);
+        beta_step<ALGO>(b, gw[j]);
+    }
+}
+
+// Window [k0, k0+len) of the backward sweep, len <= 8.  rt: this window's top
+// half inputs on entry, the next (lower) window's on exit.  st: this window's
+// bottom half on entry (LDS-DMA issued during the previous window), the next
+// window's in flight on exit.
+template <int ALGO, bool RAG, class In, class Out>
+__device__ __forceinline__ void back_window8(const In &in, const Out &out, int k0, int len, Raw (&rt)[4],
+                                             const LdsStage &st, float (&b)[NS], const float4 *ck, unsigned cs,
+                                             int lane, double sf) {
+    const int lenT = RAG ? (len > 4 ? len - 4 : 0) : 4;
+    const int lenB = RAG ? (len < 4 ? len : 4) : 4;
+    float a0[NS];
+    load_vec<true>(a0, ck, cs, (k0 / 8) * 4, lane);
+    if (!RAG || lenT > 0) {
+        float gw[4][8], lcA[4], lcB[4];
+        double iAw[4], iBw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            in.gamma(rt[j], gw[j], iAw[j], iBw[j]);
+            lcA[j] = rt[j].v.x;
+            lcB[j] = rt[j].v.y;
+        }
+        wait_vm_all();   // the staged bottom half (and the checkpoint) have landed
+        float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a4[s] = a0[s];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float g[8];
+            double x, y;
+            in.gamma(in.staged(st, i), g, x, y);
+            alpha_step<ALGO>(a4, g);
+        }
+        if (k0 > 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rt[j] = in.load(k0 - 4 + j);
+        }
+        window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
+    } else {
+        wait_vm_all();
+        if (k0 > 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rt[j] = in.load(k0 - 4 + j);
+        }
+    }
+    float gw[4][8], lcA[4], lcB[4];
+    double iAw[4], iBw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const Raw r = in.staged(st, j);
+        in.gamma(r, gw[j], iAw[j], iBw[j]);
+        lcA[j] = r.v.x;
+        lcB[j] = r.v.y;
+    }
+    if (k0 > 0) {   // the next window's bottom half, straight into LDS (the reads above are consumed)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) in.stage(k0 - 8 + j, st, j);
+    }
+    window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
+}
+
+constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16-step grid over the top 256 steps
+
+template <int ALGO, bool RAG, class In, class Out>
+__device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
+                      const LdsStage &lb) {
+    constexpr int G = 4, CK = 8;
+    const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
+    Raw raw[G];
+    float a[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) a[s] = 0.0f;
+    // F1: groups of 4 steps, inputs pipelined one group ahead, checkpoint every 8
+#pragma unroll
+    for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
+    for (int k0 = 0; k0 < N; k0 += G) {
+        float g[G][8];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            double iA, iB;
+            in.gamma(raw[j], g[j], iA, iB);
+        }
+        if (k0 + G < N) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(k0 + G + j, N - 1) : k0 + G + j);
+        }
+        if ((k0 & (CK - 1)) == 0) store_vec<true>(ck, cs, (k0 / CK) * 4, lane, a);
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
+    }
+    // F2 until merged with F1 at a checkpoint
+#pragma unroll
+    for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
+    for (int k0 = 0; k0 < N; k0 += G) {
+        const bool at_ck = (k0 & (CK - 1)) == 0;
+        if (at_ck && wave_all_equal<true>(a, ck, cs, (k0 / CK) * 4, lane)) break;
+        float g[G][8];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            double iA, iB;
+            in.gamma(raw[j], g[j], iA, iB);
+        }
+        if (k0 + G < N) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(k0 + G + j, N - 1) : k0 + G + j);
+        }
+        if (at_ck) store_vec<true>(ck, cs, (k0 / CK) * 4, lane, a);
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
+    }
+    // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
+    float b[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) b[s] = 0.0f;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            raw[j] = in.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
+            in.stage(RAG ? min(top + j, N - 1) : top + j, lb, j);
+        }
+        for (int k0 = top; k0 >= 0; k0 -= CK) {
+            const int r = (top - k0) / CK;
+            const bool keep = r % RSTEP8 == 0 && r < RING * RSTEP8;
+            if (pass == 0 && keep) store_vec<false>(ring, cs, r / RSTEP8 * 4, lane, b);   // beta1 entering
+            if (pass == 1 && keep && wave_all_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane)) break;
+            back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, lb, b, ck, cs, lane, sf);
+        }
+    }
+}
+
 // ---- kernels --------------------------------------------------------------------
 constexpr int BLOCK = 256;               // 4 waves; each wave owns one 64-codeword tile at a time
 constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 #ifndef TDEC_WIN
 #define TDEC_WIN 4
 #endif
-constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval (must divide N; every table N is a multiple of 4)
+constexpr int WIN = TDEC_WIN;            // log-MAP alpha checkpoint interval; the workspace is sized for it
+#ifndef TDEC_WIN_ML
+#define TDEC_WIN_ML 4
+#endif
+// max-log checkpoint interval: 4 (siso<>), or 8 (siso8: LDS-DMA staged half
+// windows, bit-identical).  8 moves 12 % fewer bytes (1.33 vs 1.51 MB per
+// codeword, rocprof) but ran 5 % slower on MI355X (73.7 vs 69.8 ms per
+// 262 144 codewords, tools/ab.py): the extra serial alpha steps per window
+// expose latency that two waves per SIMD do not hide.  Kept as an A/B variant
+// (python -m modulations_amd.build --variant ml8 TDEC_WIN_ML=8).
+constexpr int WIN_ML = TDEC_WIN_ML;
+__host__ __device__ constexpr int win_of(int algo) { return algo ? WIN : WIN_ML; }
+constexpr int LDS_STAGE = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of a block's staging planes
+
+// The SISO of the tile decoder: siso8 for max-log at WIN_ML 8, else siso<> at WIN.
+template <int ALGO, bool RAG, class In, class Out>
+__device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs,
+                                         int lane, double sf, float4 *lv, double2 *ll) {
+    if constexpr (ALGO == 0 && WIN_ML == 8) {
+        const int w = threadIdx.x >> 6;
+        siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{lv + w * 4 * WAVE, ll + w * 4 * WAVE, lane});
+    } else {
+        siso<ALGO, (ALGO ? WIN : WIN_ML), RAG>(in, out, N, ck, ring, cs, lane, sf);
+    }
+}
 
 // Plane layout of one 64-codeword tile ([N][64] each, codeword fastest):
 //   X[k] = {A[k], B[k], W1[k], Y1[k]}  float4   decoder 1, natural order
@@ -664,7 +911,7 @@ struct DecodeArgs {
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
 template <int ALGO, bool RAG>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
-                                                   const int *__restrict__ inv) {
+                                                   const int *__restrict__ inv, float4 *lv, double2 *ll) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
@@ -683,9 +930,10 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            siso<ALGO, WIN, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
-                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs}, N, ck, ring, rs, lane, sf);
-            siso<ALGO, WIN, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf);
+            run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
+                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs}, N, ck, ring, rs, lane, sf, lv, ll);
+            run_siso<ALGO, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf,
+                                lv, ll);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -712,7 +960,9 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_turbo_decode(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
-    turbo_decode_tiles<0, RAG>(p, perm, inv);
+    __shared__ float4 lv[LDS_STAGE];
+    __shared__ double2 ll[LDS_STAGE];
+    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll);
 }
 #ifndef TDEC_LM_WPE
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
@@ -720,7 +970,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
-    turbo_decode_tiles<1, RAG>(p, perm, inv);
+    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr);
 }
 
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).

@@ -957,8 +957,11 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 // values that do not fit go to scratch, outside the trellis loops.  log-MAP
 // spills more (its max* needs the registers), but a second wave per SIMD still
 // beats the one-wave VALU issue limit by a third.
+#ifndef TDEC_ML_WPE
+#define TDEC_ML_WPE 2
+#endif
 template <bool RAG>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_turbo_decode(
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
     __shared__ float4 lv[LDS_STAGE];
     __shared__ double2 ll[LDS_STAGE];
@@ -1148,17 +1151,21 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
                      all2[ax ^ 1] - all1[ax ^ 1] > tol;
             }
     if (!ok) return false;
+    // The half holding the overall nearest point has that point as its
+    // candidate (same first-minimum rule per axis), so its distance is shared
+    // by every bit: BPS + 1 numpy distances instead of 2 * BPS.
+    const T an = cabs_np<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
+    const T dn = an * an;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax)
 #pragma unroll
         for (int b = 0; b < K; ++b) {
+            const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
+            const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
+            const T a = cabs_np<T>(sr - lev_i[ia], si - lev_q[iq]);
             T m[2];
-#pragma unroll
-            for (int v = 0; v < 2; ++v) {
-                const int ia = ax ? allarg[0] : arg[0][b][v], iq = ax ? arg[1][b][v] : allarg[1];
-                const T a = cabs_np<T>(sr - lev_i[ia], si - lev_q[iq]);
-                m[v] = a * a;
-            }
+            m[vn] = dn;
+            m[vo] = a * a;
             out[ax * K + b] = llr_of<T>(m[0], m[1], c);
         }
     return true;

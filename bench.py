@@ -112,11 +112,12 @@ def main():
     cons = D.constellation(args.mod)
     B = args.batch
     t0 = time.time()
+    # decoder workspace and planes first, into unfragmented HBM (placement)
+    pipe = DevicePipeline(codec, args.mod, B, device)
     info, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, Sh.shard_seed(12345, rank), device)
     S = syms.shape[1]
     nv = np.float64(n0)
     f64, div32, nve = D.demap_mode(np.complex64, cons.dtype, nv)
-    pipe = DevicePipeline(codec, args.mod, B, device)
     bits = pipe.bits
     torch.cuda.synchronize()
     log(f"[rank {rank}] workload ready: {B} codewords x {S} symbols in {time.time() - t0:.1f}s")

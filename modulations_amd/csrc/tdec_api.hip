@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -198,7 +199,9 @@ struct tdec_ctx {
     int max_waves = 0;                 // resident waves of the decode kernel on this device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
-    DevBuf le, ck;                     // per-wave decode workspace
+    DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
+    double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
+    float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
     DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
     int cap_batch = 0;
@@ -308,8 +311,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_inv);
     hipFree(h->d_src);
     hipFree(h->d_off);
-    h->le.release();
-    h->ck.release();
+    h->ws.release();
     h->planes_own.release();
     h->h_llr.release();
     h->h_bits.release();
@@ -335,12 +337,84 @@ static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 static long ws_stride_of(const tdec_t *h) { return 3L * h->N * WAVE; }
 static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN - 1) / WIN + RING) * 4 * WAVE; }
 
-// Workspace for `waves` concurrently decoding waves.
+// Time one single-iteration decode of waves*64 codewords of constant LLRs on a
+// candidate workspace (the placement probe below).
+static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, const float *planes, int32_t *bits,
+                             hipEvent_t e0, hipEvent_t e1) {
+    const int B = waves * WAVE;
+    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr};
+    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
+    float best = 1e30f;
+    for (int rep = 0; rep < 2; ++rep) {
+        hipEventRecord(e0, h->stream);
+        hipLaunchKernelGGL((decode_fn)k, grid, dim3(BLOCK), 0, h->stream, a, (const int *)h->d_perm,
+                           (const int *)h->d_inv);
+        hipEventRecord(e1, h->stream);
+        if (hipEventSynchronize(e1) != hipSuccess) return 1e30f;
+        float ms = 0.0f;
+        hipEventElapsedTime(&ms, e0, e1);
+        best = std::min(best, ms);
+    }
+    return best;
+}
+
+// Workspace for `waves` concurrently decoding waves: the extrinsic planes and
+// the checkpoints in one allocation (checkpoints on the next 2 MiB boundary).
+//
+// Placement probe.  The decode rate depends on where in HBM this workspace
+// lands: on MI355X a full-size workspace (6.4 GB at N = 752) decodes either at
+// ~70 or at ~79 ms per 262 144 codewords depending on the allocation, the
+// planes' placement does not matter (tools/placement.py).  So a
+// full-GPU workspace of >= 1 GiB is allocated PROBE_CANDIDATES times, each
+// candidate times a one-iteration decode of constant LLRs, and the fastest is
+// kept (the others are freed).  Setup cost: a few hundred ms, once per
+// reserve.  TDEC_PLACEMENT_PROBE=0 turns it off.
+constexpr int PROBE_CANDIDATES = 3;
+
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
-    int rc = h->le.ensure((size_t)waves * ws_stride_of(h) * sizeof(double2));
-    if (!rc) rc = h->ck.ensure((size_t)waves * ck_stride_of(h) * sizeof(float4));
-    if (rc) return rc;
+    const size_t MB2 = 2u << 20;
+    const size_t le_bytes = (size_t)waves * ws_stride_of(h) * sizeof(double2);
+    const size_t ck_off = (le_bytes + MB2 - 1) / MB2 * MB2;
+    const size_t total = ck_off + (size_t)waves * ck_stride_of(h) * sizeof(float4);
+    const char *pe = getenv("TDEC_PLACEMENT_PROBE");
+    const bool probe = !(pe && pe[0] == '0') && waves == h->max_waves && total >= (1ul << 30);
+    if (!probe) {
+        if (int rc = h->ws.ensure(total)) return rc;
+    } else {
+        h->ws.release();
+        void *cand[PROBE_CANDIDATES] = {};
+        float ms[PROBE_CANDIDATES];
+        int n = 0;
+        for (; n < PROBE_CANDIDATES; ++n)
+            if (hipMalloc(&cand[n], total) != hipSuccess) break;
+        if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
+        int best = 0;
+        void *planes = nullptr, *bits = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const size_t pb = tdec_planes_bytes(h, waves * WAVE), bb = (size_t)waves * WAVE * 2 * h->N * sizeof(int32_t);
+        if (n > 1 && hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
+            hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+            hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) == hipSuccess) {
+            for (int i = 0; i < n; ++i) {
+                ms[i] = probe_decode_ms(h, waves, (char *)cand[i], ck_off, (const float *)planes, (int32_t *)bits, e0,
+                                        e1);
+                if (ms[i] < ms[best]) best = i;
+            }
+        }
+        hipGetLastError();
+        if (e0) hipEventDestroy(e0);
+        if (e1) hipEventDestroy(e1);
+        if (planes) hipFree(planes);
+        if (bits) hipFree(bits);
+        for (int i = 0; i < n; ++i)
+            if (i != best) hipFree(cand[i]);
+        h->ws.p = cand[best];
+        h->ws.cap = total;
+    }
+    h->le_p = (double2 *)h->ws.p;
+    h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
     h->ws_waves = waves;
     return 0;
 }
@@ -372,7 +446,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, (double2 *)h->le.p, (float4 *)h->ck.p, d_bits, d_lfinal};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
@@ -431,7 +505,7 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     HIPCHK(hipMemcpyAsync(dY, LcY, nf, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(daA, LaA, nd, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
-    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float4 *)h->ck.p, ck_stride_of(h)};
+    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
     if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);

@@ -370,7 +370,7 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, cons
 // candidate times a one-iteration decode of constant LLRs, and the fastest is
 // kept (the others are freed).  Setup cost: a few hundred ms, once per
 // reserve.  TDEC_PLACEMENT_PROBE=0 turns it off.
-constexpr int PROBE_CANDIDATES = 3;
+constexpr int PROBE_CANDIDATES = 4;
 
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
@@ -385,7 +385,7 @@ static int ensure_ws(tdec_t *h, int waves) {
     } else {
         h->ws.release();
         void *cand[PROBE_CANDIDATES] = {};
-        float ms[PROBE_CANDIDATES];
+        float ms[PROBE_CANDIDATES] = {};
         int n = 0;
         for (; n < PROBE_CANDIDATES; ++n)
             if (hipMalloc(&cand[n], total) != hipSuccess) break;
@@ -404,6 +404,8 @@ static int ensure_ws(tdec_t *h, int waves) {
             }
         }
         hipGetLastError();
+        if (getenv("TDEC_PROBE_VERBOSE"))
+            for (int i = 0; i < n; ++i) fprintf(stderr, "[tdec] placement probe %d: %.3f ms%s\n", i, ms[i], i == best ? " *" : "");
         if (e0) hipEventDestroy(e0);
         if (e1) hipEventDestroy(e1);
         if (planes) hipFree(planes);

@@ -23,9 +23,27 @@ def short(name):
     return name[:60]
 
 
+def full_size(rows, dur):
+    """Drop dispatches shorter than 30 % of the kernel's longest: the
+    decoder's one-iteration workspace placement probes (tdec_reserve) run the
+    same kernel and would otherwise dilute the per-launch averages."""
+    by = collections.defaultdict(list)
+    for r in rows:
+        by[short(r["Kernel_Name"])].append(r)
+    keep = []
+    for k, rs in by.items():
+        longest = max(dur(r) for r in rs)
+        keep += [r for r in rs if dur(r) >= 0.3 * longest]
+    return keep
+
+
+def span(r):
+    return float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+
+
 def pmc(path):
     agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
+    for r in full_size(list(csv.DictReader(open(path))), span):
         agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
@@ -33,13 +51,13 @@ def pmc(path):
 def main(src, dst, batch=1 << 20):
     batch = int(batch)
     out = {"source": src, "batch_codewords": batch, "kernels": {}}
-    stats = list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))))
-    for r in stats:
-        k = short(r["Name"])
+    trace = full_size(list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))), span)
+    durs = collections.defaultdict(list)
+    for r in trace:
+        durs[short(r["Kernel_Name"])].append(span(r) / 1e6)
+    for k, v in durs.items():
         if k.startswith("k_"):
-            out["kernels"][k] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
-                                 "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6,
-                                 "share_pct": float(r["Percentage"])}
+            out["kernels"][k] = {"calls": len(v), "avg_ms": sum(v) / len(v), "min_ms": min(v), "max_ms": max(v)}
     counters = {}
     for sub in ("fetch/f", "write/w", "sq/s", "tcc/t"):
         p = os.path.join(src, sub + "_counter_collection.csv")

@@ -95,39 +95,33 @@ static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
 /* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm
  * max(a,b) + log1p(exp(-|a-b|)), with the cut-off (|a-b| > 37 -> max) of the
  * historic _jacobian_log-22.  The correction is DEFINED as the fixed sequence of
- * f32 IEEE operations below -- Cody-Waite reduction, a degree-7 polynomial for
- * exp(-r) and a degree-10 polynomial for log1p(e), all as fused multiply-adds
- * (fmaf is correctly rounded everywhere) -- |error| < 2e-7 against the real
+ * f32 IEEE operations below -- exp(-d) = 2^-n * 2^-f from x = d*log2(e) (f = x - n
+ * exact), a degree-5 polynomial for 2^-f and log1p(e) = e * Q(e) with a degree-7 Q,
+ * all as fused multiply-adds
+ * (fmaf is correctly rounded everywhere) -- |error| < 2.5e-7 against the real
  * function.  The HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr)
  * restates it bit for bit instead of depending on two different libms. */
 static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
 {
-    const float x0 = d * 0x1.715476p+0f;                     /* d * log2(e) */
-    const int n = (int)x0;
-    const float fn = (float)n;
-    float r = fmaf(-fn, 0x1.62e400p-1f, d);                   /* Cody-Waite: d - n*ln2 */
-    r = fmaf(-fn, 0x1.7f7d1cp-20f, r);
-    float p = -0x1.2755a6p-13f;                               /* exp(-r), r in [0, ln2) */
-    p = fmaf(p, r, 0x1.5c1df6p-10f);
-    p = fmaf(p, r, -0x1.0fee9ep-7f);
-    p = fmaf(p, r, 0x1.553e2ep-5f);
-    p = fmaf(p, r, -0x1.555454p-3f);
-    p = fmaf(p, r, 0x1.fffff4p-2f);
-    p = fmaf(p, r, -0x1.000000p+0f);
-    p = fmaf(p, r, 0x1.000000p+0f);
+    const float x = d * 0x1.715476p+0f;                     /* d * log2(e) */
+    const int n = (int)x;
+    const float f = x - (float)n;                             /* exact, in [0, 1) */
+    float p = -0x1.f0ca8p-11f;                                /* 2^-f */
+    p = fmaf(p, f, 0x1.2dd26cp-7f);
+    p = fmaf(p, f, -0x1.c503aep-5f);
+    p = fmaf(p, f, 0x1.ebe33ap-3f);
+    p = fmaf(p, f, -0x1.62e3aap-1f);
+    p = fmaf(p, f, 0x1.fffffep-1f);
     const float e = ldexpf(p, -n);                            /* exp(-d) */
-    float q = -0x1.2fcf46p-9f;                                /* log1p(e), e in (0, 1] */
-    q = fmaf(q, e, 0x1.f6bac6p-7f);
-    q = fmaf(q, e, -0x1.867adcp-5f);
-    q = fmaf(q, e, 0x1.871cc6p-4f);
-    q = fmaf(q, e, -0x1.2abb7cp-3f);
-    q = fmaf(q, e, 0x1.8ccddep-3f);
-    q = fmaf(q, e, -0x1.fd82a8p-3f);
-    q = fmaf(q, e, 0x1.553044p-2f);
-    q = fmaf(q, e, -0x1.fffdc0p-2f);
+    float q = -0x1.18f998p-7f;                                /* log1p(e) / e, e in (0, 1] */
+    q = fmaf(q, e, 0x1.6a33e2p-5f);
+    q = fmaf(q, e, -0x1.b9c4c8p-4f);
+    q = fmaf(q, e, 0x1.6ba9f2p-3f);
+    q = fmaf(q, e, -0x1.f5c086p-3f);
+    q = fmaf(q, e, 0x1.54bf8p-2f);
+    q = fmaf(q, e, -0x1.fff95p-2f);
     q = fmaf(q, e, 0x1.fffffap-1f);
-    q = fmaf(q, e, 0x1.c0ced2p-31f);
-    return q;
+    return q * e;
 }
 
 static inline float jac(float a, float b)

@@ -363,14 +363,15 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, cons
 // the checkpoints in one allocation (checkpoints on the next 2 MiB boundary).
 //
 // Placement probe.  The decode rate depends on where in HBM this workspace
-// lands: on MI355X a full-size workspace (6.4 GB at N = 752) decodes either at
-// ~70 or at ~79 ms per 262 144 codewords depending on the allocation, the
-// planes' placement does not matter (tools/placement.py).  So a
-// full-GPU workspace of >= 1 GiB is allocated PROBE_CANDIDATES times, each
+// lands: on MI355X a full-size workspace (6.4 GB at N = 752) decodes anywhere
+// from ~70 to ~80 ms per 262 144 codewords depending on the allocation (the
+// first allocations of a process tend to be slow), the planes' placement does
+// not matter (tools/placement.py).  So a full-GPU workspace of
+// >= 1 GiB is allocated PROBE_CANDIDATES times (at most a third of free memory), each
 // candidate times a one-iteration decode of constant LLRs, and the fastest is
 // kept (the others are freed).  Setup cost: a few hundred ms, once per
 // reserve.  TDEC_PLACEMENT_PROBE=0 turns it off.
-constexpr int PROBE_CANDIDATES = 4;
+constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 12;
 
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
@@ -384,10 +385,15 @@ static int ensure_ws(tdec_t *h, int waves) {
         if (int rc = h->ws.ensure(total)) return rc;
     } else {
         h->ws.release();
-        void *cand[PROBE_CANDIDATES] = {};
-        float ms[PROBE_CANDIDATES] = {};
+        const char *pc = getenv("TDEC_PROBE_CANDIDATES");
+        int want = std::max(2, std::min(MAX_CANDIDATES, pc ? atoi(pc) : PROBE_CANDIDATES));
+        size_t free_b = 0, total_b = 0;   // never let the candidates take more than a third of free memory
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            want = std::max(1, std::min<int>(want, (int)(free_b / 3 / total)));
+        void *cand[MAX_CANDIDATES] = {};
+        float ms[MAX_CANDIDATES] = {};
         int n = 0;
-        for (; n < PROBE_CANDIDATES; ++n)
+        for (; n < want; ++n)
             if (hipMalloc(&cand[n], total) != hipSuccess) break;
         if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
         int best = 0;

@@ -14,6 +14,8 @@
  *     synchronous.  _dev entry points take DEVICE pointers and a hipStream_t
  *     (passed as void*), are stream-ordered, never allocate and never
  *     synchronise once tdec_reserve() has sized the workspace.
+ *   - B = 0 (an empty batch) is a no-op that returns 0; the buffers may then be
+ *     null.  B < 0 is TDEC_EINVAL.
  *   - Return 0 on success, a negative TDEC_E* code otherwise;
  *     tdec_last_error() (thread-local) says why.  No exception crosses the ABI.
  *   - A handle is bound to one device.  Calls on different handles may run

@@ -428,7 +428,8 @@ static int ensure_ws(tdec_t *h, int waves) {
 }
 
 int tdec_reserve(tdec_t *h, int max_batch) {
-    if (!h || max_batch <= 0) return fail(TDEC_EINVAL, "bad reserve");
+    if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
+    if (max_batch == 0) return 0;
     Guard g(h->device);
     int rc = ensure_ws(h, std::min(n_tiles_of(max_batch), h->max_waves));
     if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
@@ -437,7 +438,9 @@ int tdec_reserve(tdec_t *h, int max_batch) {
 }
 
 int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, float *d_planes, void *stream) {
-    if (!h || !d_llr || !d_planes || B <= 0) return fail(TDEC_EINVAL, "bad depuncture arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad depuncture arguments");
+    if (B == 0) return 0;   // an empty batch is a no-op (every batched entry point)
+    if (!d_llr || !d_planes) return fail(TDEC_EINVAL, "bad depuncture arguments");
     if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
     Guard g(h->device);
     const long total = (long)n_tiles_of(B) * h->N * WAVE;
@@ -449,7 +452,9 @@ int tdec_depuncture_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, f
 
 int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_bits, double *d_lfinal,
                            void *stream) {
-    if (!h || !d_planes || !d_bits || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (B == 0) return 0;
+    if (!d_planes || !d_bits) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
@@ -465,7 +470,8 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
 
 int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits, double *d_lfinal,
                           void *stream) {
-    if (!h || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (B == 0) return 0;
     if (B > h->cap_batch) return fail(TDEC_ECAPACITY, "batch larger than tdec_reserve()");
     int rc = tdec_depuncture_dev(h, B, d_llr, llr_stride, (float *)h->planes_own.p, stream);
     if (!rc) rc = tdec_decode_planes_dev(h, B, (const float *)h->planes_own.p, d_bits, d_lfinal, stream);
@@ -473,8 +479,10 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
 }
 
 int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32_t *bits, double *lfinal) {
-    if (!h || !llr || !bits || B <= 0) return fail(TDEC_EINVAL, "bad decode arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad decode arguments");
     if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
+    if (B == 0) return 0;
+    if (!llr || !bits) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
     int rc = tdec_reserve(h, B);
     const size_t nl = (size_t)B * llr_stride * sizeof(float), nb = (size_t)B * 2 * h->N;
@@ -494,8 +502,9 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
 
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
                     const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {
-    if (!h || B <= 0 || !LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB)
-        return fail(TDEC_EINVAL, "bad siso arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad siso arguments");
+    if (B == 0) return 0;
+    if (!LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB) return fail(TDEC_EINVAL, "bad siso arguments");
     Guard g(h->device);
     const int waves = n_tiles_of(B);
     const size_t N = h->N, nf = (size_t)B * N * sizeof(float), nd = (size_t)B * N * sizeof(double);
@@ -576,8 +585,10 @@ int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void
 
 int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
                           int bps, double noise_var, int div_f32, float *d_planes, void *stream) {
-    if (!h || !d_syms || !cons || !d_planes || B <= 0 || S <= 0) return fail(TDEC_EINVAL, "bad demap arguments");
+    if (!h || B < 0 || !cons) return fail(TDEC_EINVAL, "bad demap arguments");
     if (int rc = check_demap_args(M, bps)) return rc;
+    if (B == 0) return 0;
+    if (!d_syms || !d_planes || S <= 0) return fail(TDEC_EINVAL, "bad demap arguments");
     Guard g(h->device);
     hipStream_t st = (hipStream_t)stream;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
@@ -607,7 +618,9 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
 }
 
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream) {
-    if (!h || !d_bits || !d_coded || B <= 0) return fail(TDEC_EINVAL, "bad encode arguments");
+    if (!h || B < 0) return fail(TDEC_EINVAL, "bad encode arguments");
+    if (B == 0) return 0;
+    if (!d_bits || !d_coded) return fail(TDEC_EINVAL, "bad encode arguments");
     Guard g(h->device);
     EncodeArgs a{};
     a.B = B;

@@ -286,6 +286,8 @@ def bcjr_max_log_map_batch(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, o
         if x.shape[1] < N:
             raise IndexError(f"index {x.shape[1]} is out of bounds for axis 0 with size {x.shape[1]}")
     tabs = _t.packed_tables(next_st, out_W, out_Y, prev_st, prev_inp)
+    if N == 0:   # the reference's recursions run over range(0): empty extrinsics
+        return np.zeros((A.shape[0], 0)), np.zeros((A.shape[0], 0))
     dev = _default_device() if device is None else device
     key = (N, tabs.tobytes(), ALGOS[algo] if isinstance(algo, str) else int(algo), dev)
     h = _SISO_CACHE.get(key)

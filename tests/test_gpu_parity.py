@@ -366,3 +366,35 @@ def test_decode_ragged_block_length_through_c_abi():
     t, _ = O.trellis()
     rb = O.decode_batch(llr, n, 1, T.puncture_matrix(punct), 8, perm, inv, t)
     assert np.array_equal(bits, rb)
+
+
+def test_empty_batches_are_no_ops():
+    """B = 0 through every batched entry point returns empty results, as numpy
+    would for an empty leading axis; N = 0 SISO returns empty extrinsics, as the
+    reference's recursions over range(0) do; B < 0 is rejected."""
+    import ctypes
+    from modulations_amd import _native as NT
+    c = M.DVBRCS2_Turbo(212, "1/3")
+    assert c.decode_batch(np.zeros((0, c.n_coded), np.float32)).shape == (0, c.k_info)
+    bits, lf = c.decode_batch(np.zeros((0, c.n_coded), np.float32), return_lfinal=True)
+    assert bits.shape == lf.shape == (0, c.k_info)
+    with pytest.raises(IndexError):   # the row-length check still applies to an empty batch
+        c.decode_batch(np.zeros((0, c.n_coded - 1), np.float32))
+    LeA, LeB = M.bcjr_max_log_map_batch(*np.zeros((4, 0, 48), np.float32), *np.zeros((2, 0, 48)), *_tabs(), 48, 0.7)
+    assert LeA.shape == LeB.shape == (0, 48)
+    LeA, LeB = M.bcjr_max_log_map(*np.zeros((4, 0), np.float32), *np.zeros((2, 0)), *_tabs(), 0, 0.7)
+    assert LeA.shape == LeB.shape == (0,) and LeA.dtype == np.float64
+    dl = torch.zeros((0, c.n_coded), dtype=torch.float32, device="cuda")
+    assert c.decode_device(dl).shape == (0, c.k_info)
+    u8 = torch.zeros((0, c.k_info), dtype=torch.uint8, device="cuda")
+    assert c.encode_device(u8).shape[0] == 0
+    cons = D.constellation("16QAM")
+    planes = torch.empty(16, dtype=torch.float32, device="cuda")
+    c.demap_planes_device(torch.zeros((0, 1128), dtype=torch.complex64, device="cuda"), cons, 4, 0.1, planes)
+    c.decode_planes_device(planes, 0, torch.empty((0, c.k_info), dtype=torch.int32, device="cuda"))
+    assert D.compute_llr(np.zeros(0, np.complex64), "16QAM", 0.1).size == 0
+    torch.cuda.synchronize()
+    h = c.handle.h
+    assert NT.lib().tdec_decode_batch(h, -1, None, c.n_coded, None, None) == -1
+    assert NT.lib().tdec_siso_batch(h, -1, *[None] * 6, ctypes.c_double(0.7), None, None) == -1
+    assert NT.lib().tdec_reserve(h, -1) == -1

@@ -100,6 +100,23 @@ int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, cons
 int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M,
                int bps, double noise_var, int div_f32, int sign, double *llr);
 
+/* The fixed-signature demapper of SURVEY §8(b) over the reference's built-in
+ * Gray constellations (BPSK/QPSK/8PSK/16QAM: test_sdr_with_coding.py:25-100;
+ * 64QAM/256QAM: sdr_modem.py:168-207): compute_llr(syms, mod, noise_var)
+ * (:200-225) of n_sym complex64 symbols (host f32 pairs) with noise_var given
+ * as a Python float would be, then rounded to f32 as decode() rounds its input
+ * (dvb_rcs2_turbo.py:466).  sign +1 = reference sign, -1 = decoder sign.
+ * llr_out: float[n_sym * bps]. */
+enum { TDEC_MOD_BPSK = 0, TDEC_MOD_QPSK = 1, TDEC_MOD_8PSK = 2, TDEC_MOD_16QAM = 3, TDEC_MOD_64QAM = 4,
+       TDEC_MOD_256QAM = 5 };
+int tdec_demap_batch(int device, int mod, int sign, const float *syms_iq, long n_sym, float noise_var,
+                     float *llr_out);
+/* The label-ordered table of a built-in constellation (what compute_llr builds,
+ * :207-208): M points as (re, im) double pairs in iq[2*M]; *is_f64 = 1 when
+ * numpy's table is complex128 (QPSK), else every value is a float32.
+ * Returns M, or a negative TDEC_E* code.  Host only (no device call). */
+int tdec_constellation(int mod, double *iq, int *is_f64);
+
 /* Fused demap -> de-puncture for the decoder: B codewords of S complex64
  * symbols each ([B][S]); LLR j of a codeword = bit j of its symbol stream
  * (zero-padded / truncated to the decoder's LLR count as

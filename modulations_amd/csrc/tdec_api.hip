@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -638,3 +639,89 @@ int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, v
 }
 
 }  // extern "C"
+
+// ---- built-in Gray constellations and the fixed-signature demapper --------------------
+// The label-ordered tables compute_llr builds (test_sdr_with_coding.py:207-208)
+// from the reference mappers, with numpy's arithmetic and result dtype:
+//   BPSK   2.0 * complex64(b) - 1.0                       (:25-26)          complex64
+//   QPSK   complex64(1-2b0 + j(1-2b1)) / np.sqrt(2)        (:31-37)          complex128
+//          (numpy divides by the complex128 scalar sqrt(2)+0j with Smith's
+//          method: re * (1 / sqrt(2)))
+//   8PSK   exp(j * GRAY3[label] * pi / 4) -> complex64    (:45-57)
+//   QAM    (2*gray[i] - (L-1)) / sqrt(scale) per axis     (:72-86, sdr_modem.py:142-207) complex64
+static int builtin_constellation(int mod, double *iq, int *is_f64) {
+    static const int g2[4] = {0, 1, 3, 2}, g3[8] = {0, 1, 3, 2, 6, 7, 5, 4},
+                     g4[16] = {0, 1, 3, 2, 6, 7, 5, 4, 12, 13, 15, 14, 10, 11, 9, 8};
+    *is_f64 = 0;
+    switch (mod) {
+    case TDEC_MOD_BPSK:
+        for (int i = 0; i < 2; ++i) {
+            iq[2 * i] = (double)(2.0f * (float)i - 1.0f);
+            iq[2 * i + 1] = 0.0;
+        }
+        return 2;
+    case TDEC_MOD_QPSK: {
+        *is_f64 = 1;
+        const double scl = 1.0 / (std::sqrt(2.0) + 0.0 * 0.0);
+        for (int i = 0; i < 4; ++i) {
+            const double re = 1 - 2 * (i >> 1), im = 1 - 2 * (i & 1);
+            iq[2 * i] = (re + im * 0.0) * scl;
+            iq[2 * i + 1] = (im - re * 0.0) * scl;
+        }
+        return 4;
+    }
+    case TDEC_MOD_8PSK:
+        for (int i = 0; i < 8; ++i) {
+            const double p = g3[i] * M_PI / 4;
+            iq[2 * i] = (double)(float)std::cos(p);
+            iq[2 * i + 1] = (double)(float)std::sin(p);
+        }
+        return 8;
+    case TDEC_MOD_16QAM:
+    case TDEC_MOD_64QAM:
+    case TDEC_MOD_256QAM: {
+        const int k = mod == TDEC_MOD_16QAM ? 2 : (mod == TDEC_MOD_64QAM ? 3 : 4);
+        const int L = 1 << k, scale = k == 2 ? 10 : (k == 3 ? 42 : 170);
+        const int *g = k == 2 ? g2 : (k == 3 ? g3 : g4);
+        const double sq = std::sqrt((double)scale);
+        for (int i = 0; i < L * L; ++i) {
+            iq[2 * i] = (double)(float)((double)(2 * g[i >> k] - (L - 1)) / sq);
+            iq[2 * i + 1] = (double)(float)((double)(2 * g[i & (L - 1)] - (L - 1)) / sq);
+        }
+        return L * L;
+    }
+    default: return fail(TDEC_EINVAL, "unknown modulation id");
+    }
+}
+
+int tdec_constellation(int mod, double *iq, int *is_f64) {
+    if (!iq || !is_f64) return fail(TDEC_EINVAL, "null argument");
+    return builtin_constellation(mod, iq, is_f64);
+}
+
+int tdec_demap_batch(int device, int mod, int sign, const float *syms_iq, long n_sym, float noise_var,
+                     float *llr_out) {
+    double tab[512];
+    int f64 = 0;
+    const int M = builtin_constellation(mod, tab, &f64);
+    if (M < 0) return M;
+    if (n_sym < 0 || (sign != 1 && sign != -1)) return fail(TDEC_EINVAL, "bad demap arguments");
+    int bps = 0;
+    while ((1 << bps) < M) ++bps;
+    if (n_sym == 0) return 0;
+    if (!syms_iq || !llr_out) return fail(TDEC_EINVAL, "bad demap arguments");
+    std::vector<float> t32;
+    const void *cons = tab;
+    if (!f64) {   // complex64 table
+        t32.assign(tab, tab + 2 * M);
+        cons = t32.data();
+    }
+    // compute_llr with a Python-float noise_var: the final division stays
+    // float32 unless the arithmetic is complex128 (QPSK)
+    const double nv = (double)noise_var;
+    std::vector<double> l64((size_t)n_sym * bps);
+    const int rc = tdec_demap(device, syms_iq, 0, n_sym, cons, f64, M, bps, nv, !f64, sign, l64.data());
+    if (rc) return rc;
+    for (size_t i = 0; i < l64.size(); ++i) llr_out[i] = (float)l64[i];   // decode()'s f32 cast (:466)
+    return 0;
+}

@@ -42,3 +42,22 @@ def test_no_silent_cpu_path_without_gpu():
     c = DVBRCS2_Turbo(48, "1/3")
     with pytest.raises(_native.TdecError):
         c.decode(np.zeros(c.n_coded))
+
+
+def test_builtin_constellations_match_the_mapper_tables():
+    """tdec_constellation (host only) rebuilds the label-ordered tables that
+    compute_llr gets from the reference mappers, value and dtype exact."""
+    import ctypes as C
+    import numpy as np
+    from modulations_amd import demap as D
+    L = _native.lib()
+    for mod_id, name in enumerate(("BPSK", "QPSK", "8PSK", "16QAM", "64QAM", "256QAM")):
+        iq = np.zeros(512)
+        f64 = C.c_int(-1)
+        M = L.tdec_constellation(mod_id, _native.ptr(iq), C.byref(f64))
+        want = D.constellation(name)
+        assert M == len(want), name
+        assert bool(f64.value) == (want.dtype == np.complex128), name
+        got = iq[0:2 * M:2] + 1j * iq[1:2 * M:2]
+        assert np.array_equal(got, want.astype(np.complex128)), name
+    assert L.tdec_constellation(6, _native.ptr(np.zeros(512)), C.byref(C.c_int())) == _native.TDEC_EINVAL

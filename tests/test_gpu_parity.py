@@ -398,3 +398,25 @@ def test_empty_batches_are_no_ops():
     assert NT.lib().tdec_decode_batch(h, -1, None, c.n_coded, None, None) == -1
     assert NT.lib().tdec_siso_batch(h, -1, *[None] * 6, ctypes.c_double(0.7), None, None) == -1
     assert NT.lib().tdec_reserve(h, -1) == -1
+
+
+@pytest.mark.parametrize("mod", ["BPSK", "QPSK", "8PSK", "16QAM", "64QAM", "256QAM"])
+def test_demap_batch_fixed_signature(mod):
+    """tdec_demap_batch (SURVEY §8(b) signature) = compute_llr with a Python-float
+    noise_var, rounded to f32, in either sign convention."""
+    from modulations_amd import _native as NT
+    rng = np.random.default_rng(7)
+    cons = D.constellation(mod)
+    n = 3001
+    syms = (cons[rng.integers(0, len(cons), n)] + 0.3 * (rng.standard_normal(n) + 1j * rng.standard_normal(n)))
+    syms = syms.astype(np.complex64)
+    bps = D.MODULATIONS[mod]["bps"]
+    mod_id = ("BPSK", "QPSK", "8PSK", "16QAM", "64QAM", "256QAM").index(mod)
+    for sign in (1, -1):
+        out = np.zeros(n * bps, np.float32)
+        NT.check(NT.lib().tdec_demap_batch(0, mod_id, sign, NT.ptr(syms), n, 0.125, NT.ptr(out)))
+        want = (sign * D.compute_llr(syms, mod, 0.125)).astype(np.float32)
+        assert np.array_equal(out, want), (mod, sign)
+        if sign == 1:   # and the oracle, on the same f32 table / dtype rules
+            _, div32, nve = D.demap_mode(np.complex64, cons.dtype, 0.125)
+            assert np.array_equal(out, O.demap(syms, cons, bps, nve, div_f32=div32).astype(np.float32))

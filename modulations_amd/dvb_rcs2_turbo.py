@@ -25,6 +25,7 @@ path; the batched device encoder is ``encode_device``).
 from __future__ import annotations
 
 import ctypes as C
+import sys
 
 import numpy as np
 
@@ -61,11 +62,16 @@ class _Handle:
         self.llr_len = _n.lib().tdec_llr_len(h)
         self.enc_len = _n.lib().tdec_encoded_len(h)
 
-    def __del__(self):
+    def __del__(self, _finalizing=sys.is_finalizing):
+        # at interpreter exit the process releases the device anyway, and the
+        # module globals this would need may already be gone
         h = getattr(self, "h", None)
-        if h is not None and h.value and _n._lib is not None:
-            _n._lib.tdec_destroy(h)
-            self.h = None
+        if h is None or not h.value or _finalizing():
+            return
+        lib = getattr(_n, "_lib", None) if _n is not None else None
+        if lib is not None:
+            lib.tdec_destroy(h)
+        self.h = None
 
 
 def _default_device():

@@ -300,6 +300,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     const long row_units = std::max<long>(N, 4L * ((N + WIN - 1) / WIN + RING));
     const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
     h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
+    // experiment knob: run the persistent decoder on a percentage of the resident waves
+    if (const char *pw = getenv("TDEC_WAVES_PCT")) {
+        const int pct = std::max(1, std::min(100, atoi(pw)));
+        h->max_waves = std::max(WAVES_PER_BLOCK, h->max_waves * pct / 100 / WAVES_PER_BLOCK * WAVES_PER_BLOCK);
+    }
     *out = h;
     return TDEC_OK;
 }

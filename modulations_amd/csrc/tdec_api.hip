@@ -373,11 +373,16 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, cons
 // from ~70 to ~80 ms per 262 144 codewords depending on the allocation (the
 // first allocations of a process tend to be slow), the planes' placement does
 // not matter (tools/placement.py).  So a full-GPU workspace of
-// >= 1 GiB is allocated PROBE_CANDIDATES times (at most a third of free memory), each
-// candidate times a one-iteration decode of constant LLRs, and the fastest is
-// kept (the others are freed).  Setup cost: a few hundred ms, once per
-// reserve.  TDEC_PLACEMENT_PROBE=0 turns it off.
-constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 12;
+// >= 1 GiB is allocated PROBE_CANDIDATES times, each candidate times a
+// one-iteration decode of constant LLRs, and the fastest is kept (the others
+// are freed).  The candidate times are bimodal: a fast placement probes >= 3 %
+// below the median of its round; when the best of a round is not (every
+// candidate slow; seen in 1 of 6 fresh processes) another round of candidates
+// is allocated while the first ones are still held, up to MAX_CANDIDATES and
+// half of the free memory.  Setup cost: a few hundred ms, once per reserve.
+// TDEC_PLACEMENT_PROBE=0 turns it off.
+constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 16;
+constexpr float FAST_VS_MEDIAN = 0.97f;
 
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
@@ -392,28 +397,40 @@ static int ensure_ws(tdec_t *h, int waves) {
     } else {
         h->ws.release();
         const char *pc = getenv("TDEC_PROBE_CANDIDATES");
-        int want = std::max(2, std::min(MAX_CANDIDATES, pc ? atoi(pc) : PROBE_CANDIDATES));
-        size_t free_b = 0, total_b = 0;   // never let the candidates take more than a third of free memory
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
-            want = std::max(1, std::min<int>(want, (int)(free_b / 3 / total)));
+        const int per_round = std::max(2, std::min(MAX_CANDIDATES, pc ? atoi(pc) : PROBE_CANDIDATES));
+        int cap = MAX_CANDIDATES;
+        size_t free_b = 0, total_b = 0;   // never let the candidates take more than half of free memory
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::max(1, std::min<int>(cap, (int)(free_b / 2 / total)));
         void *cand[MAX_CANDIDATES] = {};
         float ms[MAX_CANDIDATES] = {};
-        int n = 0;
-        for (; n < want; ++n)
-            if (hipMalloc(&cand[n], total) != hipSuccess) break;
-        if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
-        int best = 0;
+        int n = 0, best = 0;
         void *planes = nullptr, *bits = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         const size_t pb = tdec_planes_bytes(h, waves * WAVE), bb = (size_t)waves * WAVE * 2 * h->N * sizeof(int32_t);
-        if (n > 1 && hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
-            hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
-            hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) == hipSuccess) {
-            for (int i = 0; i < n; ++i) {
+        bool timed = false;
+        for (int round = 0; round < 2; ++round) {
+            const int first = n, want = std::min(cap, first + (round ? per_round : std::min(per_round, cap / 2 + 1)));
+            for (; n < want; ++n)
+                if (hipMalloc(&cand[n], total) != hipSuccess) break;
+            if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
+            if (n == 1) break;
+            if (!timed) {
+                timed = hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
+                        hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+                        hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) ==
+                            hipSuccess;
+                if (!timed) break;
+            }
+            for (int i = first; i < n; ++i) {
                 ms[i] = probe_decode_ms(h, waves, (char *)cand[i], ck_off, (const float *)planes, (int32_t *)bits, e0,
                                         e1);
                 if (ms[i] < ms[best]) best = i;
             }
+            float sorted[MAX_CANDIDATES];
+            std::copy(ms + first, ms + n, sorted);
+            std::sort(sorted, sorted + (n - first));
+            const float median = sorted[(n - first) / 2];
+            if (ms[best] <= FAST_VS_MEDIAN * median || n >= cap || n == first) break;   // a fast one, or no room
         }
         hipGetLastError();
         if (getenv("TDEC_PROBE_VERBOSE"))

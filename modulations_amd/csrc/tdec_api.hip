@@ -501,25 +501,38 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
     return rc;
 }
 
+// Host-pointer decode in chunks, so device memory stays bounded for any B:
+// by default 4 x the resident-wave capacity (524 288 codewords on MI355X,
+// ~20 GB of LLR rows and planes); TDEC_HOST_CHUNK overrides it (tests use a
+// small value to exercise the chunk loop).
 int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32_t *bits, double *lfinal) {
     if (!h || B < 0) return fail(TDEC_EINVAL, "bad decode arguments");
     if (llr_stride < h->llr_len) return fail(TDEC_ESHORT, "llr rows shorter than the de-puncture walk");
     if (B == 0) return 0;
     if (!llr || !bits) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
-    int rc = tdec_reserve(h, B);
-    const size_t nl = (size_t)B * llr_stride * sizeof(float), nb = (size_t)B * 2 * h->N;
-    if (!rc) rc = h->h_llr.ensure(nl);
-    if (!rc) rc = h->h_bits.ensure(nb * sizeof(int32_t));
-    if (!rc && lfinal) rc = h->h_lf.ensure(nb * sizeof(double));
+    long chunk = 4L * h->max_waves * WAVE;
+    if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
+    const int C = (int)std::min<long>(B, chunk);
+    int rc = tdec_reserve(h, C);
+    const size_t row_b = (size_t)2 * h->N;
+    if (!rc) rc = h->h_llr.ensure((size_t)C * llr_stride * sizeof(float));
+    if (!rc) rc = h->h_bits.ensure((size_t)C * row_b * sizeof(int32_t));
+    if (!rc && lfinal) rc = h->h_lf.ensure((size_t)C * row_b * sizeof(double));
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h->h_llr.p, llr, nl, hipMemcpyHostToDevice, h->stream));
-    rc = tdec_decode_batch_dev(h, B, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
-                               lfinal ? (double *)h->h_lf.p : nullptr, h->stream);
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(bits, h->h_bits.p, nb * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
-    if (lfinal) HIPCHK(hipMemcpyAsync(lfinal, h->h_lf.p, nb * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    for (long b0 = 0; b0 < B; b0 += C) {
+        const int n = (int)std::min<long>(C, B - b0);
+        const size_t nl = (size_t)n * llr_stride * sizeof(float), nb = (size_t)n * row_b;
+        HIPCHK(hipMemcpyAsync(h->h_llr.p, llr + b0 * llr_stride, nl, hipMemcpyHostToDevice, h->stream));
+        rc = tdec_decode_batch_dev(h, n, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
+                                   lfinal ? (double *)h->h_lf.p : nullptr, h->stream);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(bits + b0 * row_b, h->h_bits.p, nb * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+        if (lfinal)
+            HIPCHK(hipMemcpyAsync(lfinal + b0 * row_b, h->h_lf.p, nb * sizeof(double), hipMemcpyDeviceToHost,
+                                  h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+    }
     return 0;
 }
 

@@ -420,3 +420,18 @@ def test_demap_batch_fixed_signature(mod):
         if sign == 1:   # and the oracle, on the same f32 table / dtype rules
             _, div32, nve = D.demap_mode(np.complex64, cons.dtype, 0.125)
             assert np.array_equal(out, O.demap(syms, cons, bps, nve, div_f32=div32).astype(np.float32))
+
+
+def test_host_decode_in_chunks(monkeypatch):
+    """tdec_decode_batch walks a large host batch in chunks (bounded device
+    memory); a small TDEC_HOST_CHUNK forces several chunks and a ragged last
+    one, results identical to the oracle."""
+    monkeypatch.setenv("TDEC_HOST_CHUNK", "70")
+    rng = np.random.default_rng(21)
+    c = M.DVBRCS2_Turbo(48, "1/2")
+    _, llr = _awgn_llrs(rng, c, 229, 1.5, 0.5)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    t, _ = O.trellis()
+    rb, rl = O.decode_batch(llr, 48, c.punct["period"], T.puncture_matrix(c.punct), 8, c.perm, c.inv_perm, t,
+                            want_lfinal=True)
+    assert np.array_equal(bits, rb) and np.array_equal(lf, rl)

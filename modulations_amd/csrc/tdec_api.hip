@@ -542,33 +542,40 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     if (B == 0) return 0;
     if (!LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB) return fail(TDEC_EINVAL, "bad siso arguments");
     Guard g(h->device);
-    const int waves = n_tiles_of(B);
-    const size_t N = h->N, nf = (size_t)B * N * sizeof(float), nd = (size_t)B * N * sizeof(double);
+    // rows in chunks, like tdec_decode_batch: device memory stays bounded for any B
+    long chunk = 4L * h->max_waves * WAVE;
+    if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
+    const int C = (int)std::min<long>(B, chunk), waves = n_tiles_of(C);
+    const size_t N = h->N, cf = (size_t)C * N * sizeof(float), cd = (size_t)C * N * sizeof(double);
     int rc = ensure_ws(h, waves);
-    if (!rc) rc = h->h_misc.ensure(4 * nf + 4 * nd);
+    if (!rc) rc = h->h_misc.ensure(4 * cf + 4 * cd);
     if (rc) return rc;
     char *base = (char *)h->h_misc.p;
-    float *dA = (float *)base, *dB = (float *)(base + nf), *dW = (float *)(base + 2 * nf), *dY = (float *)(base + 3 * nf);
-    double *daA = (double *)(base + 4 * nf), *daB = (double *)(base + 4 * nf + nd);
-    double *deA = (double *)(base + 4 * nf + 2 * nd), *deB = (double *)(base + 4 * nf + 3 * nd);
+    float *dA = (float *)base, *dB = (float *)(base + cf), *dW = (float *)(base + 2 * cf), *dY = (float *)(base + 3 * cf);
+    double *daA = (double *)(base + 4 * cf), *daB = (double *)(base + 4 * cf + cd);
+    double *deA = (double *)(base + 4 * cf + 2 * cd), *deB = (double *)(base + 4 * cf + 3 * cd);
     hipStream_t s = h->stream;
-    HIPCHK(hipMemcpyAsync(dA, LcA, nf, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(dB, LcB, nf, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(dW, LcW, nf, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(dY, LcY, nf, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(daA, LaA, nd, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(daB, LaB, nd, hipMemcpyHostToDevice, s));
-    SisoArgs a{B, h->N, waves, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
-    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
-    if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
-    else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
-    else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
-    else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(LeA, deA, nd, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(LeB, deB, nd, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    for (long r0 = 0; r0 < B; r0 += C) {
+        const int n = (int)std::min<long>(C, B - r0), nwv = n_tiles_of(n);
+        const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(float), nd = (size_t)n * N * sizeof(double);
+        HIPCHK(hipMemcpyAsync(dA, LcA + o, nf, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dB, LcB + o, nf, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dW, LcW + o, nf, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dY, LcY + o, nf, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(daA, LaA + o, nd, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
+        SisoArgs a{n, h->N, nwv, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
+        const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+        if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
+        else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
+        else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
+        else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(LeA + o, deA, nd, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(LeB + o, deB, nd, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     return 0;
 }
 

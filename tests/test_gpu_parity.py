@@ -423,9 +423,9 @@ def test_demap_batch_fixed_signature(mod):
 
 
 def test_host_decode_in_chunks(monkeypatch):
-    """tdec_decode_batch walks a large host batch in chunks (bounded device
-    memory); a small TDEC_HOST_CHUNK forces several chunks and a ragged last
-    one, results identical to the oracle."""
+    """tdec_decode_batch and tdec_siso_batch walk a large host batch in chunks
+    (bounded device memory); a small TDEC_HOST_CHUNK forces several chunks and
+    a ragged last one, results identical to the oracle."""
     monkeypatch.setenv("TDEC_HOST_CHUNK", "70")
     rng = np.random.default_rng(21)
     c = M.DVBRCS2_Turbo(48, "1/2")
@@ -435,3 +435,11 @@ def test_host_decode_in_chunks(monkeypatch):
     rb, rl = O.decode_batch(llr, 48, c.punct["period"], T.puncture_matrix(c.punct), 8, c.perm, c.inv_perm, t,
                             want_lfinal=True)
     assert np.array_equal(bits, rb) and np.array_equal(lf, rl)
+    n, B = 50, 151
+    Lc = (rng.standard_normal((4, B, n)) * 4).astype(np.float32)
+    La = rng.standard_normal((2, B, n)) * 9
+    M._SISO_CACHE.clear()
+    LeA, LeB = M.bcjr_max_log_map_batch(*Lc, *La, *_tabs(), n, 0.7)
+    for b in (0, 69, 70, 139, 140, 150):
+        rA, rB = O.siso(*Lc[:, b], *La[:, b], t, 0.7)
+        assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b

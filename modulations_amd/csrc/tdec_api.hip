@@ -132,6 +132,12 @@ struct ConsCache {
     std::vector<double> host;
     bool f64 = false;
     int sep = 0, nbps = -1;
+    bool matches(const void *cons, int cons_f64, int M, int bps, bool want_f64) const {
+        if (!buf.p || f64 != want_f64 || nbps != bps || (int)host.size() != 2 * M) return false;
+        for (int i = 0; i < 2 * M; ++i)
+            if (host[i] != (cons_f64 ? ((const double *)cons)[i] : (double)((const float *)cons)[i])) return false;
+        return true;
+    }
     int upload(const void *cons, int cons_f64, int M, int bps, bool want_f64, hipStream_t st) {
         std::vector<double> d(2 * M);
         for (int i = 0; i < 2 * M; ++i)
@@ -210,7 +216,50 @@ struct tdec_ctx {
     ConsCache cons;                    // demapper constellation
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // copies of the chunked host-pointer path (created on first use)
+    // Stream ordering of the handle-owned buffers (workspace, planes_own, cons,
+    // staging): every call that touches them records done_ev on the stream it
+    // ran on; a later call on a different stream waits on it first, so a
+    // decode_device() on one stream followed by a decode_batch() (private
+    // stream) or a _dev call on another stream cannot overwrite buffers a
+    // running kernel still reads.
+    hipEvent_t done_ev = nullptr;
+    hipStream_t last_st = nullptr;
+    bool pending = false;
 };
+
+namespace {
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+// host-side wait for the last queued use (before buffers are regrown or staged)
+void quiesce(tdec_ctx *h) {
+    if (h->pending) hipEventSynchronize(h->done_ev);
+}
+// make stream s wait for the last use of the handle's buffers (on another stream)
+int order_on(tdec_ctx *h, hipStream_t s) {
+    if (h->pending && h->last_st != s && !capturing(s)) HIPCHK(hipStreamWaitEvent(s, h->done_ev, 0));
+    return 0;
+}
+// the handle's buffers are in use by work queued on s
+int mark_used(tdec_ctx *h, hipStream_t s) {
+    if (capturing(s)) return 0;   // under stream capture the caller orders the graph
+    HIPCHK(hipEventRecord(h->done_ev, s));
+    h->last_st = s;
+    h->pending = true;
+    return 0;
+}
+// On every exit of a host-pointer entry point: the copies queued on the
+// handle's streams read / write the caller's host buffers, so they must have
+// finished before the caller gets control back (errors included).
+struct DrainOnExit {
+    hipStream_t a, b;
+    ~DrainOnExit() {
+        if (a) hipStreamSynchronize(a);
+        if (b && b != a) hipStreamSynchronize(b);
+    }
+};
+}  // namespace
 
 extern "C" {
 
@@ -286,6 +335,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMemcpy(h->d_inv, inv_perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_src, src.data(), sizeof(int32_t) * 8 * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->done_ev, hipEventDisableTiming);
     int blocks_per_cu = 0, n_cu = 0;
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -314,6 +364,7 @@ void tdec_destroy(tdec_t *h) {
     if (!h) return;
     Guard g(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->pending) hipEventSynchronize(h->done_ev);
     hipFree(h->d_perm);
     hipFree(h->d_inv);
     hipFree(h->d_src);
@@ -327,6 +378,7 @@ void tdec_destroy(tdec_t *h) {
     h->cons.buf.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
+    if (h->done_ev) hipEventDestroy(h->done_ev);
     delete h;
 }
 
@@ -456,7 +508,9 @@ int tdec_reserve(tdec_t *h, int max_batch) {
     if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
     if (max_batch == 0) return 0;
     Guard g(h->device);
-    int rc = ensure_ws(h, std::min(n_tiles_of(max_batch), h->max_waves));
+    const int want_waves = std::min(n_tiles_of(max_batch), h->max_waves);
+    if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);   // regrowth frees
+    int rc = ensure_ws(h, want_waves);
     if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
     if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
     return rc;
@@ -487,10 +541,12 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, (hipStream_t)stream,
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = order_on(h, st)) return rc;
+    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, st,
                        a, pm, iv);
     HIPCHK(hipGetLastError());
-    return 0;
+    return mark_used(h, st);
 }
 
 int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits, double *d_lfinal,
@@ -498,6 +554,7 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
     if (!h || B < 0) return fail(TDEC_EINVAL, "bad decode arguments");
     if (B == 0) return 0;
     if (B > h->cap_batch) return fail(TDEC_ECAPACITY, "batch larger than tdec_reserve()");
+    if (int rc = order_on(h, (hipStream_t)stream)) return rc;   // planes_own may still be read elsewhere
     int rc = tdec_depuncture_dev(h, B, d_llr, llr_stride, (float *)h->planes_own.p, stream);
     if (!rc) rc = tdec_decode_planes_dev(h, B, (const float *)h->planes_own.p, d_bits, d_lfinal, stream);
     return rc;
@@ -506,7 +563,7 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
 // Host-pointer decode in chunks, so device memory stays bounded for any B:
 // by default half the resident-wave capacity (65 536 codewords on MI355X:
 // the path is PCIe-bound, so small chunks that pipeline well beat large ones,
-// 1.07 M vs 0.70 M codewords/s at 262 144); TDEC_HOST_CHUNK overrides it
+// 1.21 M vs 0.70 M codewords/s at 262 144); TDEC_HOST_CHUNK overrides it
 // (tests use a small value to exercise the chunk loop).  With several chunks the copies run
 // on a second stream into two alternating buffers, and the next chunk's H2D is
 // issued before this chunk's D2H (which blocks the host for pageable memory),
@@ -530,6 +587,7 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     if (B == 0) return 0;
     if (!llr || !bits) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
+    quiesce(h);   // earlier _dev work on other streams may still use the buffers staged below
     long chunk = std::max(1L, (long)h->max_waves / 2) * WAVE;
     if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
     const int C = (int)std::min<long>(B, chunk);
@@ -543,6 +601,7 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     if (rc) return rc;
     if (nbuf == 2 && !h->cstream) HIPCHK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
     hipStream_t cs = nbuf == 2 ? h->cstream : h->stream;
+    DrainOnExit drain{h->stream, cs};   // declared before the events: they die after the drain
     EventPair up, dec;
     if ((rc = up.create()) || (rc = dec.create())) return rc;
     float *dl = (float *)h->h_llr.p;
@@ -584,6 +643,8 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     if (B == 0) return 0;
     if (!LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB) return fail(TDEC_EINVAL, "bad siso arguments");
     Guard g(h->device);
+    quiesce(h);
+    DrainOnExit drain{h->stream, nullptr};
     // rows in chunks, like tdec_decode_batch: device memory stays bounded for any B
     long chunk = 4L * h->max_waves * WAVE;
     if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
@@ -618,7 +679,7 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
         HIPCHK(hipMemcpyAsync(LeB + o, deB, nd, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
     }
-    return 0;
+    return mark_used(h, s);
 }
 
 int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M,
@@ -627,10 +688,30 @@ int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, cons
     if (int rc = check_demap_args(M, bps)) return rc;
     if (n_sym == 0) return 0;
     Guard g(device);
-    static thread_local ConsCache tbl[16];
-    ConsCache &cc = tbl[device & 15];
     const bool f64 = sym_f64 || cons_f64;
     hipStream_t st = (hipStream_t)stream;
+    // Tables are cached per (thread, device) by content and never overwritten
+    // while another stream may still read them: a new table takes a fresh slot;
+    // only when all slots are taken is the oldest reused, after a device-wide
+    // synchronisation.
+    constexpr int SLOTS = 8;
+    static thread_local std::vector<ConsCache> tbl[16];
+    static thread_local int next_victim[16];
+    std::vector<ConsCache> &v = tbl[device & 15];
+    if (v.empty()) v.reserve(SLOTS);
+    ConsCache *hit = nullptr;
+    for (auto &c : v)
+        if (c.matches(cons, cons_f64, M, bps, f64)) hit = &c;
+    if (!hit) {
+        if ((int)v.size() < SLOTS) {
+            v.emplace_back();
+            hit = &v.back();
+        } else {
+            HIPCHK(hipDeviceSynchronize());
+            hit = &v[next_victim[device & 15]++ % SLOTS];
+        }
+    }
+    ConsCache &cc = *hit;
     if (int rc = cc.upload(cons, cons_f64, M, bps, f64, st)) return rc;
     DevBuf &tb = cc.buf;
     DemapCfg c{M, div_f32, sign, (0.005 > noise_var) ? 0.005 : noise_var, cc.sep};
@@ -676,6 +757,7 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (!d_syms || !d_planes || S <= 0) return fail(TDEC_EINVAL, "bad demap arguments");
     Guard g(h->device);
     hipStream_t st = (hipStream_t)stream;
+    if (int rc = order_on(h, st)) return rc;   // the table below may still be read on another stream
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
     DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep};
     const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
@@ -699,7 +781,7 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     default: return fail(TDEC_EINVAL, "bps must be 1..8");
     }
     HIPCHK(hipGetLastError());
-    return 0;
+    return mark_used(h, st);
 }
 
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream) {

@@ -137,9 +137,16 @@ def compute_llr_device(syms, mod_type, noise_var, out=None, sign=+1, stream=None
     n_sym = syms.numel() // (1 if syms.is_complex() else 2)
     f64, div_f32, nv = demap_mode(np.complex128 if sym_f64 else np.complex64, cons.dtype, noise_var)
     c = np.ascontiguousarray(cons.astype(np.complex128 if f64 else np.complex64))
+    if syms.device.type != "cuda" or not syms.is_contiguous():
+        raise ValueError("syms must be a contiguous tensor on a HIP device")
+    if syms.dtype not in (torch.complex64, torch.complex128, torch.float32, torch.float64):
+        raise TypeError(f"unsupported symbol dtype {syms.dtype}")
+    dev = syms.device.index or 0
     if out is None:
         out = torch.empty(n_sym * m['bps'], dtype=torch.float64, device=syms.device)
-    _n.check(_n.lib().tdec_demap_dev(syms.device.index or 0, _n.ptr(syms), int(sym_f64), n_sym, _n.ptr(c), int(f64),
-                                     len(c), m['bps'], nv, int(div_f32), int(sign), _n.ptr(out),
-                                     _n.stream_ptr(stream)))
+    if out.dtype != torch.float64 or not out.is_contiguous() or out.numel() < n_sym * m['bps'] or out.device != syms.device:
+        raise ValueError("out must be a contiguous float64 tensor of n_sym*bps elements on the symbols' device")
+    st = _n.stream_ptr(stream) if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    _n.check(_n.lib().tdec_demap_dev(dev, _n.ptr(syms), int(sym_f64), n_sym, _n.ptr(c), int(f64),
+                                     len(c), m['bps'], nv, int(div_f32), int(sign), _n.ptr(out), st))
     return out

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import ctypes as C
 import sys
+import threading
 
 import numpy as np
 
@@ -47,7 +48,13 @@ def _std_tables():
 
 
 class _Handle:
-    """Owns one tdec_t (device-side codec state)."""
+    """Owns one tdec_t (device-side codec state).
+
+    A tdec_t's staging buffers, workspace and private streams are shared by
+    every call on it, and ctypes releases the GIL during a call, so calls on
+    one handle are serialised by ``lock`` (``call``): the module-level caches
+    hand the same handle to every Python thread, as the reference functions
+    may be called from several threads at once."""
 
     def __init__(self, device, n, punct, iterations, algo, perm, inv_perm, tables):
         pm = np.ascontiguousarray(_t.puncture_matrix(punct))
@@ -61,6 +68,12 @@ class _Handle:
         self.device = device
         self.llr_len = _n.lib().tdec_llr_len(h)
         self.enc_len = _n.lib().tdec_encoded_len(h)
+        self.lock = threading.Lock()
+
+    def call(self, name, *args):
+        """lib().<name>(self.h, *args) under the handle lock, errors raised."""
+        with self.lock:
+            return _n.check(getattr(_n.lib(), name)(self.h, *args))
 
     def __del__(self, _finalizing=sys.is_finalizing):
         # at interpreter exit the process releases the device anyway, and the
@@ -191,35 +204,77 @@ class DVBRCS2_Turbo:
         bits = np.zeros((B, self.k_info), np.int32)
         lf = np.zeros((B, self.k_info)) if return_lfinal else None
         if B:
-            _n.check(_n.lib().tdec_decode_batch(h.h, B, _n.ptr(llr), llr.shape[1], _n.ptr(bits), _n.ptr(lf)))
+            h.call("tdec_decode_batch", B, _n.ptr(llr), llr.shape[1], _n.ptr(bits), _n.ptr(lf))
         return (bits, lf) if return_lfinal else bits
 
     # -- device-resident API (torch tensors on this codec's GPU) -------------------------
     def reserve(self, max_batch):
-        _n.check(_n.lib().tdec_reserve(self.handle.h, int(max_batch)))
+        self.handle.call("tdec_reserve", int(max_batch))
 
     def planes_bytes(self, B):
         return _n.lib().tdec_planes_bytes(self.handle.h, int(B))
 
-    def decode_device(self, llr, bits=None, lfinal=None, stream=None):
-        """llr: float32 [B, n] device tensor -> int32 [B, 2N] device tensor."""
+    # -- argument checks of the device wrappers: a wrong dtype, stride, shape or
+    #    device would otherwise mean silently wrong data or out-of-bounds writes
+    def _dev_check(self, t, name, dtype, shape=None, rows_contig=False):
         import torch
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda" or t.device.index != self.device:
+            raise ValueError(f"{name} must be a tensor on cuda:{self.device}")
+        if t.dtype != dtype:
+            raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+        if rows_contig:
+            if t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1) or (t.shape[0] > 1 and t.stride(0) < t.shape[1]):
+                raise ValueError(f"{name} rows must be contiguous (stride(1) == 1)")
+        elif not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+    def _stream(self, stream):
+        """The caller's stream, or torch's current stream on this codec's device."""
+        if stream is not None:
+            return _n.stream_ptr(stream)
+        import torch
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def decode_device(self, llr, bits=None, lfinal=None, stream=None):
+        """llr: float32 [B, n] device tensor (rows contiguous) -> int32 [B, 2N] device tensor.
+        Stream-ordered on `stream` (default: torch's current stream)."""
+        import torch
+        self._dev_check(llr, "llr", torch.float32, rows_contig=True)
         B = llr.shape[0]
+        if B and llr.shape[1] < self.handle.llr_len:
+            raise IndexError(f"index {llr.shape[1]} is out of bounds for axis 0 with size {llr.shape[1]}")
         self.reserve(B)
         if bits is None:
             bits = torch.empty((B, self.k_info), dtype=torch.int32, device=llr.device)
-        _n.check(_n.lib().tdec_decode_batch_dev(self.handle.h, B, _n.ptr(llr), llr.stride(0), _n.ptr(bits),
-                                                _n.ptr(lfinal), _n.stream_ptr(stream)))
+        self._dev_check(bits, "bits", torch.int32, (B, self.k_info))
+        if lfinal is not None:
+            self._dev_check(lfinal, "lfinal", torch.float64, (B, self.k_info))
+        self.handle.call("tdec_decode_batch_dev", B, _n.ptr(llr), llr.stride(0) if B > 1 else llr.shape[1],
+                         _n.ptr(bits), _n.ptr(lfinal), self._stream(stream))
         return bits
 
     def decode_planes_device(self, planes, B, bits, lfinal=None, stream=None):
-        _n.check(_n.lib().tdec_decode_planes_dev(self.handle.h, B, _n.ptr(planes), _n.ptr(bits), _n.ptr(lfinal),
-                                                 _n.stream_ptr(stream)))
+        import torch
+        if planes.numel() * planes.element_size() < self.planes_bytes(B):
+            raise ValueError("planes buffer smaller than planes_bytes(B)")
+        self._dev_check(planes, "planes", torch.float32)
+        self._dev_check(bits, "bits", torch.int32, (B, self.k_info))
+        if lfinal is not None:
+            self._dev_check(lfinal, "lfinal", torch.float64, (B, self.k_info))
+        self.handle.call("tdec_decode_planes_dev", B, _n.ptr(planes), _n.ptr(bits), _n.ptr(lfinal),
+                         self._stream(stream))
         return bits
 
     def depuncture_device(self, llr, planes, stream=None):
-        _n.check(_n.lib().tdec_depuncture_dev(self.handle.h, llr.shape[0], _n.ptr(llr), llr.stride(0),
-                                              _n.ptr(planes), _n.stream_ptr(stream)))
+        import torch
+        self._dev_check(llr, "llr", torch.float32, rows_contig=True)
+        self._dev_check(planes, "planes", torch.float32)
+        if planes.numel() * 4 < self.planes_bytes(llr.shape[0]):
+            raise ValueError("planes buffer smaller than planes_bytes(B)")
+        self.handle.call("tdec_depuncture_dev", llr.shape[0], _n.ptr(llr),
+                         llr.stride(0) if llr.shape[0] > 1 else llr.shape[1], _n.ptr(planes), self._stream(stream))
         return planes
 
     def demap_planes_device(self, syms, constellation, bps, noise_var, planes, div_f32=False, stream=None):
@@ -227,20 +282,25 @@ class DVBRCS2_Turbo:
         cons = np.ascontiguousarray(np.asarray(constellation))
         f64 = cons.dtype == np.complex128
         cons = cons.astype(np.complex128 if f64 else np.complex64)
+        import torch
+        self._dev_check(syms, "syms", torch.complex64)
+        self._dev_check(planes, "planes", torch.float32)
         B, S = syms.shape[0], syms.shape[1]
-        _n.check(_n.lib().tdec_demap_planes_dev(self.handle.h, B, _n.ptr(syms), S, _n.ptr(cons), int(f64),
-                                                len(cons), bps, float(noise_var), int(div_f32), _n.ptr(planes),
-                                                _n.stream_ptr(stream)))
+        if planes.numel() * 4 < self.planes_bytes(B):
+            raise ValueError("planes buffer smaller than planes_bytes(B)")
+        self.handle.call("tdec_demap_planes_dev", B, _n.ptr(syms), S, _n.ptr(cons), int(f64), len(cons), bps,
+                         float(noise_var), int(div_f32), _n.ptr(planes), self._stream(stream))
         return planes
 
     def encode_device(self, bits_u8, coded_u8=None, stream=None):
         """Batched device encoder: uint8 [B, 2N] -> uint8 [B, n_out] (same bits as encode())."""
         import torch
+        self._dev_check(bits_u8, "bits", torch.uint8, (bits_u8.shape[0], self.k_info))
         B = bits_u8.shape[0]
         if coded_u8 is None:
             coded_u8 = torch.empty((B, self.handle.enc_len), dtype=torch.uint8, device=bits_u8.device)
-        _n.check(_n.lib().tdec_encode_dev(self.handle.h, B, _n.ptr(bits_u8), _n.ptr(coded_u8),
-                                          _n.stream_ptr(stream)))
+        self._dev_check(coded_u8, "coded", torch.uint8, (B, self.handle.enc_len))
+        self.handle.call("tdec_encode_dev", B, _n.ptr(bits_u8), _n.ptr(coded_u8), self._stream(stream))
         return coded_u8
 
 
@@ -262,6 +322,7 @@ class DVB_RCS2_TurboCodec(DVBRCS2_Turbo):
 # ---- module-level functions of the reference ------------------------------------------
 
 _SISO_CACHE = {}
+_CACHE_LOCK = threading.Lock()
 
 
 def bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,
@@ -296,16 +357,16 @@ def bcjr_max_log_map_batch(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, o
         return np.zeros((A.shape[0], 0)), np.zeros((A.shape[0], 0))
     dev = _default_device() if device is None else device
     key = (N, tabs.tobytes(), ALGOS[algo] if isinstance(algo, str) else int(algo), dev)
-    h = _SISO_CACHE.get(key)
-    if h is None:
-        ident = np.arange(N, dtype=np.int32)
-        h = _Handle(dev, N, PUNCTURE_PATTERNS['1/3'], 1, key[2], ident, ident, tabs)
-        _SISO_CACHE[key] = h
+    with _CACHE_LOCK:
+        h = _SISO_CACHE.get(key)
+        if h is None:
+            ident = np.arange(N, dtype=np.int32)
+            h = _SISO_CACHE[key] = _Handle(dev, N, PUNCTURE_PATTERNS['1/3'], 1, key[2], ident, ident, tabs)
     B = A.shape[0]
     LeA = np.zeros((B, N))
     LeB = np.zeros((B, N))
-    _n.check(_n.lib().tdec_siso_batch(h.h, B, _n.ptr(A), _n.ptr(Bv), _n.ptr(W), _n.ptr(Y), _n.ptr(la), _n.ptr(lb),
-                                      float(scaling_factor), _n.ptr(LeA), _n.ptr(LeB)))
+    h.call("tdec_siso_batch", B, _n.ptr(A), _n.ptr(Bv), _n.ptr(W), _n.ptr(Y), _n.ptr(la), _n.ptr(lb),
+           float(scaling_factor), _n.ptr(LeA), _n.ptr(LeB))
     return LeA, LeB
 
 
@@ -315,8 +376,10 @@ _CODEC_CACHE = {}
 def turbo_decode(llr, N_couples, code_rate, iterations=8, **kw):
     """Historic module-level decode: DVBRCS2_Turbo(...).decode(llr)."""
     key = (N_couples, code_rate, iterations, tuple(sorted(kw.items())))
-    c = _CODEC_CACHE.get(key)
-    if c is None:
-        c = _CODEC_CACHE[key] = DVBRCS2_Turbo(N_couples, code_rate, iterations, **kw)
+    with _CACHE_LOCK:
+        c = _CODEC_CACHE.get(key)
+        if c is None:
+            c = _CODEC_CACHE[key] = DVBRCS2_Turbo(N_couples, code_rate, iterations, **kw)
+        h = c.handle   # created under the lock: one handle per cached codec
     llr = np.asarray(llr)
     return c.decode_batch(llr) if llr.ndim == 2 else c.decode(llr)

@@ -7,38 +7,114 @@ on): 16-QAM soft-LLR demap + DVB-RCS2 duo-binary turbo decode, N = 752 couples
 of the hot path over one batch of synthetic codewords already resident in
 HBM: fused demap + de-puncture (k_demap_planes) followed by the fused turbo
 decoder (k_turbo_decode), hard bits out.  Inputs are generated on the device
-(random info bits -> device encoder -> Gray 16-QAM -> complex AWGN) before
-the timed region.
+before the timed region by the counter-based generator (Philox info bits of
+global codeword indices -> device encoder -> Gray 16-QAM -> complex AWGN).
 
-Multi-GPU: one process per GPU (torchrun); every rank decodes its own shard
-of codewords (weak scaling, no data-path collective); the barrier /
-max-over-ranks timing and the error counters use torch.distributed.
+Multi-GPU: one process per GPU.  `--gpus N` run as a plain `python bench.py`
+spawns the N rank processes itself (the parent never touches the GPU); under
+torchrun (WORLD_SIZE set) every process is already one rank.  Each rank
+decodes its own contiguous range of global codewords (weak scaling, no
+data-path collective); the barrier, the max-over-ranks time and the error
+counters use torch.distributed (RCCL on the node).
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from modulations_amd import demap as D  # noqa: E402
-from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402
-from modulations_amd import sharding as Sh  # noqa: E402
-from modulations_amd.workload import DevicePipeline, make_symbols  # noqa: E402
-
-VALU_PEAK = 256 * 4 * 32 * 2.4e9     # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_PEAK = 256 * 4 * 32 * 2.4e9     # lane-ops/s: 256 CU x 4 SIMD-32 x 2.4 GHz, a wave64 per 2 cycles (MI355X_MICROARCH.md)
 HBM_PEAK = 8.0e12                    # B/s (spec)
+SEED = 12345
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU per step")
+    ap.add_argument("--ebn0", type=float, default=2.0)
+    ap.add_argument("--mod", default="16QAM")
+    ap.add_argument("--n", type=int, default=752)
+    ap.add_argument("--rate", default="1/3")
+    ap.add_argument("--algo", default="max-log")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
+                    "several ranks on one GPU together with --all-on-device0")
+    ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
+    return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N`: start N rank processes (one per GPU) and wait.
+    Nothing in this parent initialises HIP; the children are fresh processes."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    for q in procs:        # one rank failed: the others would wait at a barrier forever
+                        q.kill()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+def lib_sha256():
+    from modulations_amd import _native
+    with open(_native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def measured_traffic(workload, kernel):
+    """rocprof HBM bytes per codeword of `kernel` for this workload, only when
+    profiles/traffic.json was measured on the exact library that is loaded."""
+    tf = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(tf):
+        return None, "no profiles/traffic.json"
+    ent = json.load(open(tf)).get(kernel, {}).get(workload)
+    if not ent:
+        return None, "workload not profiled"
+    if ent.get("lib_sha256") != lib_sha256():
+        return None, "profiles/traffic.json was measured on another libtdec.so build"
+    return ent, None
 
 
 def cpu_baseline(codec, syms_host, cons, bps, nv, div32, seconds):
@@ -54,7 +130,7 @@ def cpu_baseline(codec, syms_host, cons, bps, nv, div32, seconds):
     def run(rows, nthreads=threads):
         llr = np.stack([-O.demap(s, cons, bps, nv, div_f32=div32)[:codec.n_coded] for s in rows]).astype(np.float32)
         return O.decode_batch(llr, codec.N, codec.punct["period"], pm, codec.iterations, codec.perm,
-                              codec.inv_perm, t, nthreads=nthreads)
+                              codec.inv_perm, t, algo=codec.algo, nthreads=nthreads)
 
     t0 = time.perf_counter()
     run(syms_host[:threads])
@@ -67,54 +143,56 @@ def cpu_baseline(codec, syms_host, cons, bps, nv, div32, seconds):
     t0 = time.perf_counter()
     run(syms_host[:n1], 1)
     dt1 = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "codewords/s", "cores": threads, "kind": "port",
-            "sample": f"{n} codewords of the same workload (oracle demap + decode, OpenMP over codewords on "
-                      f"{threads} threads), {dt:.1f} s; single core: {n1} codewords, {dt1:.1f} s",
-            "info_bits_per_s": n * codec.k_info / dt, "single_core_value": n1 / dt1}
+    out = {"value": n / dt, "unit": "codewords/s", "cores": threads, "kind": "port",
+           "sample": f"{n} codewords of the same workload (oracle demap + decode, OpenMP over codewords on "
+                     f"{threads} threads), {dt:.1f} s; single core: {n1} codewords, {dt1:.1f} s",
+           "info_bits_per_s": n * codec.k_info / dt, "single_core_value": n1 / dt1}
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        out["numba_ratio"] = c["ratio_1core"]
+        out["numba_calibration"] = (f"the C restatement decodes {c['oracle_1t_cw_per_s']:.0f} cw/s on one core of the "
+                                    f"survey's container vs the reference's numba machine code at "
+                                    f"{c['numba_1core_cw_per_s']:.0f} cw/s there (SURVEY.md §6; N=752 r=1/3 decode "
+                                    f"only): ratio {c['ratio_1core']:.2f} (profiles/cpu_calibration.json)")
+    return out
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="codewords per GPU per step")
-    ap.add_argument("--ebn0", type=float, default=2.0)
-    ap.add_argument("--mod", default="16QAM")
-    ap.add_argument("--n", type=int, default=752)
-    ap.add_argument("--rate", default="1/3")
-    ap.add_argument("--algo", default="max-log")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
-                    "several ranks on one GPU together with --all-on-device0")
-    ap.add_argument("--all-on-device0", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    from modulations_amd import demap as D
+    from modulations_amd import dvb_rcs2_turbo as M
+    from modulations_amd import sharding as Sh
+    from modulations_amd.workload import DevicePipeline, count_errors, make_symbols
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    tdist = None
+    dev_idx = 0 if args.all_on_device0 else local
+    torch.cuda.set_device(dev_idx)
     if dist:
         import torch.distributed as tdist
-        dev_idx = 0 if args.all_on_device0 else local
-        torch.cuda.set_device(dev_idx)
         if args.dist_backend == "nccl":
             tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
             tdist.init_process_group(args.dist_backend)
-    else:
-        torch.cuda.set_device(0)
-    device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device("cuda", dev_idx)
 
     codec = M.DVBRCS2_Turbo(args.n, args.rate, 8, algo=args.algo, device=device.index)
     bps = D.MODULATIONS[args.mod]["bps"]
     cons = D.constellation(args.mod)
     B = args.batch
+    cw0 = rank * B                                   # this rank's global codewords: [rank*B, (rank+1)*B)
     t0 = time.time()
     # decoder workspace and planes first, into unfragmented HBM (placement)
     pipe = DevicePipeline(codec, args.mod, B, device)
-    info, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, Sh.shard_seed(12345, rank), device)
+    _, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, SEED, device, cw0=cw0, want_info=False)
     S = syms.shape[1]
     nv = np.float64(n0)
     f64, div32, nve = D.demap_mode(np.complex64, cons.dtype, nv)
@@ -143,34 +221,33 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t_start
-    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))   # k_turbo_decode launch duration
+    # k_turbo_decode launch duration: events recorded on the stream the kernel runs on
+    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed:.3f}s, decode kernel {dec_ms:.2f} ms/launch")
 
-    # error counters (not timed): info-bit errors, frame errors, codewords
-    errs = (bits.to(torch.uint8) != info).sum(dim=1)
+    # error counters (not timed): info-bit errors, frame errors, codewords, against the generator's bits
+    errs = count_errors(codec, bits, SEED, cw0=cw0)
     red_dev = device if (not dist or args.dist_backend == "nccl") else torch.device("cpu")
-    cnt = torch.tensor([int(errs.sum()), int((errs > 0).sum()), B], dtype=torch.int64, device=red_dev)
+    cnt = torch.tensor([int(errs.sum(dtype=torch.int64)), int((errs > 0).sum()), B], dtype=torch.int64,
+                       device=red_dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    Sh.reduce_counters(cnt, tdist if dist else None)
-    Sh.reduce_max(tmax, tdist if dist else None)
+    dmax = torch.tensor([dec_ms], dtype=torch.float64, device=red_dev)
+    Sh.reduce_counters(cnt, tdist)
+    Sh.reduce_max(tmax, tdist)
+    Sh.reduce_max(dmax, tdist)
     elapsed = float(tmax)
     total_cw = B * world * args.steps
     value = total_cw / elapsed
 
     if rank == 0:
-        n_llr = codec.n_coded
-        alg_bytes = B * (4 * n_llr + 4 * codec.k_info)        # f32 LLRs in + int32 bits out per codeword
-        achieved = alg_bytes / (dec_ms * 1e-3)
-        ops = 2 * codec.iterations * codec.N * 768            # SURVEY §8(d) lane-op count per codeword
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic.json")
         wl = (f"{args.mod} soft-LLR demap + DVB-RCS2 turbo N={args.n} couples ({2 * args.n} info bits) "
               f"r={args.rate}, 8 it {args.algo}-MAP")
-        if os.path.exists(tf):
-            tr = json.load(open(tf)).get("k_turbo_decode", {})
-            if tr.get("workload") == wl:
-                traffic = tr["hbm_bytes_per_codeword"] * B      # measured HBM bytes per launch (rocprof PMC)
-        valu_achieved = B * ops / (dec_ms * 1e-3)
+        kname = "k_turbo_decode_logmap" if codec.algo else "k_turbo_decode"
+        ops = 2 * codec.iterations * codec.N * 768            # SURVEY §8(d) lane-op count per codeword
+        valu_achieved = B * ops / (dec_ms * 1e-3)              # per GPU: this rank's launch
+        alg_bytes = B * (4 * codec.n_coded + 4 * codec.k_info)  # f32 LLRs in + int32 bits out per codeword
+        tr, why = measured_traffic(wl, kname)
+        traffic = tr["hbm_bytes_per_codeword"] * B if tr else None
         out = {
             "metric": "codewords/sec + info-bits/sec, N=1504 r=1/3 8-iter max-log-MAP @1/2/4/8 GPU",
             "value": value,
@@ -184,51 +261,60 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 (recursions) / f64 (branch sums, extrinsic)",
-            "data": "synthetic (device-generated info bits -> encoder -> Gray 16QAM -> AWGN)",
-            "config": {"workload": f"{args.mod} soft-LLR demap + DVB-RCS2 turbo N={args.n} couples "
-                                   f"({2 * args.n} info bits) r={args.rate}, 8 it {args.algo}-MAP",
-                       "codewords_per_gpu_per_step": B, "ebn0_db": args.ebn0,
+            "data": "synthetic (device counter-based generator: Philox info bits -> encoder -> Gray "
+                    f"{args.mod} -> AWGN)",
+            "config": {"workload": wl, "codewords_per_gpu_per_step": B, "ebn0_db": args.ebn0,
                        "parallelism": f"codeword shards x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_turbo_decode", "achieved": achieved / 1e9,
-                         "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                         "traffic": traffic,
-                         "traffic_GBps": (traffic / (dec_ms * 1e-3) / 1e9) if traffic else None,
-                         "note": "achieved = algorithmic bytes (4*n_coded f32 LLRs in + 4*2N int32 bits out per "
-                                 "codeword) / k_turbo_decode launch time; traffic = rocprof-measured HBM bytes per "
-                                 "launch (profiles/traffic.json): the per-lane decoder streams its alpha "
-                                 "checkpoints, a-priori and branch inputs through HBM on every pass, and that "
-                                 "stream (traffic_GBps) is what bounds it"},
-            "valu": {"achieved": valu_achieved / 1e12, "peak": VALU_PEAK / 1e12, "unit": "T lane-op/s",
-                     "frac": valu_achieved / VALU_PEAK, "ops_per_codeword": ops},
+            "roofline": {
+                "bound": "valu", "kernel": kname,
+                "achieved": valu_achieved / 1e12, "peak": VALU_PEAK / 1e12, "unit": "T lane-op/s",
+                "frac": valu_achieved / VALU_PEAK,
+                "traffic": traffic,
+                "note": "SURVEY §8(d): the recursions are VALU issue work, W = 2*I*N*768 f32 lane-ops per codeword "
+                        f"({ops}); achieved = W x codewords per launch / k_turbo_decode launch time (HIP events "
+                        "on its stream); peak = 256 CU x 4 SIMD-32 x 2.4 GHz (a wave64 VALU op per 2 cycles). "
+                        "traffic = rocprof-measured HBM bytes per launch (profiles/traffic.json, used only when "
+                        "stamped with the sha256 of the loaded libtdec.so)",
+            },
+            "hbm": {
+                "algorithmic_GBps": alg_bytes / (dec_ms * 1e-3) / 1e9, "peak_GBps": HBM_PEAK / 1e9,
+                "algorithmic_frac": alg_bytes / (dec_ms * 1e-3) / HBM_PEAK,
+                "algorithmic_bytes_per_codeword": alg_bytes / B,
+                "measured_bytes_per_codeword": tr["hbm_bytes_per_codeword"] if tr else None,
+                "measured_GBps": (traffic / (dec_ms * 1e-3) / 1e9) if traffic else None,
+                "measured_source": tr.get("source") if tr else why,
+            },
             "decode_kernel_ms": dec_ms,
-            "ber": {"bit_errors": int(cnt[0]), "frame_errors": int(cnt[1]), "codewords": int(cnt[2]), "info_ber": int(cnt[0]) / (int(cnt[2]) * codec.k_info)},
+            "decode_kernel_ms_max_over_ranks": float(dmax),
+            "ber": {"bit_errors": int(cnt[0]), "frame_errors": int(cnt[1]), "codewords": int(cnt[2]),
+                    "info_ber": int(cnt[0]) / (int(cnt[2]) * codec.k_info)},
         }
         if world == 1 and not args.no_cpu:
             # PCIe-inclusive rate of the host-pointer drop-in boundary (DVBRCS2_Turbo.decode_batch):
             # host f32 LLRs in, host int32 bits out, same codec and kernels (informational, never `value`)
             hb = min(B, 262144)
-            rows = (1.0 - 2.0 * np.random.default_rng(1).integers(0, 2, (1024, codec.n_coded))).astype(np.float32) * 2.0
-            llr_h = np.ascontiguousarray(np.tile(rows, (-(-hb // 1024), 1))[:hb])
+            k = min(B, 80000)
+            syms_host = syms[:k].cpu().numpy()
+            from oracle import oracle as O
+            llr_rows = np.stack([-O.demap(s, cons, bps, nve, div_f32=div32)[:codec.n_coded]
+                                 for s in syms_host[:1024]]).astype(np.float32)
+            llr_h = np.ascontiguousarray(np.tile(llr_rows, (-(-hb // 1024), 1))[:hb])
             codec.decode_batch(llr_h)                 # steady state: staging buffers already sized
             t0 = time.perf_counter()
             codec.decode_batch(llr_h)
             dt = time.perf_counter() - t0
             out["host_api"] = {"value": hb / dt, "unit": "codewords/s", "batch": hb,
-                               "path": "DVBRCS2_Turbo.decode_batch(numpy f32 [B, n_coded]) -> numpy int32, "
-                                       "H2D + depuncture + decode + D2H in pipelined chunks of 65536"}
-            k = min(B, 80000)
-            syms_host = syms[:k].cpu().numpy()
+                               "path": "DVBRCS2_Turbo.decode_batch(numpy f32 [B, n_coded], pageable; the bench's "
+                                       "own noisy LLRs, 1024 distinct rows tiled) -> numpy int32, H2D + depuncture "
+                                       "+ decode + D2H in pipelined chunks of 65536"}
             log("[rank 0] timing the CPU baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline(codec, syms_host, cons, bps, nve, div32, args.cpu_seconds)
             # parity spot-check of the timed GPU output against the oracle on the same sample
-            from oracle import oracle as O
             from modulations_amd import tables as T
             t, _ = O.trellis()
             chk = 64
-            llr = np.stack([-O.demap(s, cons, bps, nve, div_f32=div32)[:codec.n_coded]
-                            for s in syms_host[:chk]]).astype(np.float32)
-            rb = O.decode_batch(llr, codec.N, codec.punct["period"], T.puncture_matrix(codec.punct), 8, codec.perm,
-                                codec.inv_perm, t)
+            rb = O.decode_batch(llr_rows[:chk], codec.N, codec.punct["period"], T.puncture_matrix(codec.punct), 8,
+                                codec.perm, codec.inv_perm, t, algo=codec.algo)
             out["parity_spot_check"] = bool(np.array_equal(bits[:chk].cpu().numpy(), rb))
         print(json.dumps(out), flush=True)
     if dist:

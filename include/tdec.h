@@ -131,6 +131,28 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream);
 long tdec_encoded_len(const tdec_t *h);
 
+/* ---- counter-based workload generation (not a reference API) ----
+ * Codeword c of a batch has the GLOBAL index cw0 + c; its info bits and its
+ * channel noise are Philox4x32-10 streams keyed by `seed` and counted by that
+ * index, so they do not depend on the batch or the number of ranks a job is
+ * sharded over.  Info bit j of codeword g is bit j%32 of word (j%128)/32 of
+ * philox4x32_10({g_lo, g_hi, j/128, 0x1AF0}, {seed_lo, seed_hi}).
+ * Needs n_couples % 4 == 0 and n_couples <= 1024 (every DVB-RCS2 block size). */
+
+/* info bits -> encode (as tdec_encode_dev) -> label-ordered constellation
+ * (cons_iq: M host (re, im) float pairs, label = bps coded bits MSB first, the
+ * last symbol zero-padded) -> complex AWGN of std-dev sigma per dimension
+ * (Box-Muller on philox4x32_10({g_lo, g_hi, s/2, 0x2B0E}, seed)).  d_syms:
+ * complex64 [B][ceil(n_out / bps)]; d_info (nullable): uint8 [B][2N]. */
+int tdec_workload_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const float *cons_iq, int M, int bps,
+                      double sigma, float *d_syms, uint8_t *d_info, void *stream);
+/* The info bits alone: uint8 [B][2N] of 0/1. */
+int tdec_info_bits_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, uint8_t *d_info, void *stream);
+/* Bit errors per codeword of decoded rows (int32 [B][2N], tdec_decode_*) against
+ * those info bits: d_errs int32 [B]. */
+int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const int32_t *d_bits, int32_t *d_errs,
+                          void *stream);
+
 #ifdef __cplusplus
 }
 #endif

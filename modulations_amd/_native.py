@@ -26,7 +26,7 @@ EXPORTS = (
     "tdec_create", "tdec_destroy", "tdec_last_error", "tdec_llr_len", "tdec_siso_batch", "tdec_decode_batch",
     "tdec_reserve", "tdec_planes_bytes", "tdec_depuncture_dev", "tdec_decode_planes_dev", "tdec_decode_batch_dev",
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
-    "tdec_demap_batch", "tdec_constellation",
+    "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
 )
 
 _lib = None
@@ -63,13 +63,18 @@ def _declare(L):
     L.tdec_encode_dev.argtypes = [_vp, C.c_int, _vp, _vp, _vp]
     L.tdec_demap_batch.argtypes = [C.c_int, C.c_int, C.c_int, _vp, C.c_long, C.c_float, _vp]
     L.tdec_constellation.argtypes = [C.c_int, _vp, C.POINTER(C.c_int)]
+    L.tdec_workload_dev.argtypes = [_vp, C.c_int, C.c_int64, C.c_uint64, _vp, C.c_int, C.c_int, C.c_double, _vp,
+                                    _vp, _vp]
+    L.tdec_info_bits_dev.argtypes = [_vp, C.c_int, C.c_int64, C.c_uint64, _vp, _vp]
+    L.tdec_count_errors_dev.argtypes = [_vp, C.c_int, C.c_int64, C.c_uint64, _vp, _vp, _vp]
     for name in EXPORTS:
         f = getattr(L, name)
         if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",
                                             "tdec_depuncture_dev", "tdec_decode_planes_dev",
                                             "tdec_decode_batch_dev", "tdec_demap_dev", "tdec_demap",
                                             "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_demap_batch",
-                                            "tdec_constellation"):
+                                            "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev",
+                                            "tdec_count_errors_dev"):
             f.restype = C.c_int
 
 

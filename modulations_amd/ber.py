@@ -5,10 +5,12 @@ Eb/N0 points x codewords, sharded over GPUs with torchrun, resumable.
       --codewords 10000000 --out ber_256qam.json
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m modulations_amd.ber ...
 
-Each rank owns a contiguous codeword range per point (sharding.shard_range),
-generates it on its own device from a per-(rank, point) seed, runs the fused
-demap + decode, and counts bit / frame errors; only those int64 counters are
-all-reduced.  Finished points are written to --out after every point, and a
+Each rank owns a contiguous range of global codeword indices per point
+(sharding.shard_range) and generates it on its own device with the
+counter-based generator (seed per point, counter = global codeword index: the
+data, and so the counters, are the same for any world size or batch size),
+runs the fused demap + decode, and counts bit / frame errors on the device;
+only those int64 counters are all-reduced.  Finished points are written to --out after every point, and a
 rerun skips them (checkpoint / resume).
 """
 from __future__ import annotations
@@ -28,21 +30,21 @@ def parse_points(spec):
     return [float(x) for x in spec.split(",")]
 
 
-def run_point(pipe, codec, mod, ebn0, count, batch, seed, device):
+def run_point(pipe, codec, mod, ebn0, start, count, batch, seed, device):
+    """Bit errors, frame errors and codewords of global codewords
+    [start, start + count) at one Eb/N0 point.  The data of codeword g is a
+    counter-based stream of (seed, g) (workload.make_symbols), so the counters
+    do not depend on the batch size or on how the job is sharded."""
     import torch
     from . import sharding as S
+    from .workload import count_errors, make_symbols
     cnt = torch.zeros(3, dtype=torch.int64, device=device)
-    for i, (off, n) in enumerate(S.batches(count, batch)):
-        info, syms, n0 = _gen(codec, n, mod, ebn0, seed + i, device)
+    for off, n in S.batches(count, batch):
+        _, syms, n0 = make_symbols(codec, n, mod, ebn0, seed, device, cw0=start + off, want_info=False)
         bits = pipe.run(syms, n0)[:n]
-        e = (bits.to(torch.uint8) != info).sum(dim=1)
-        cnt += torch.stack([e.sum(), (e > 0).sum(), torch.tensor(n, device=device)]).to(torch.int64)
+        e = count_errors(codec, bits, seed, cw0=start + off)
+        cnt += torch.stack([e.sum(dtype=torch.int64), (e > 0).sum(), torch.tensor(n, device=device)]).to(torch.int64)
     return cnt
-
-
-def _gen(codec, n, mod, ebn0, seed, device):
-    from .workload import make_symbols
-    return make_symbols(codec, n, mod, ebn0, seed, device)
 
 
 def main(argv=None):
@@ -54,7 +56,7 @@ def main(argv=None):
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--mod", default="256QAM")
-    ap.add_argument("--n", type=int, default=752)
+    ap.add_argument("--n", "--couples", dest="n", type=int, default=752)
     ap.add_argument("--rate", default="1/3")
     ap.add_argument("--algo", default="max-log")
     ap.add_argument("--iterations", type=int, default=8)
@@ -64,15 +66,21 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--interleaver", default="reference")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse")
+    ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_idx = 0 if a.all_on_device0 else local
+    torch.cuda.set_device(dev_idx)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", torch.cuda.current_device())
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(a.dist_backend)
+    device = torch.device("cuda", dev_idx)
     codec = M.DVBRCS2_Turbo(a.n, a.rate, a.iterations, algo=a.algo, interleaver=a.interleaver,
                             device=device.index)
     pipe = DevicePipeline(codec, a.mod, a.batch, device)
@@ -85,7 +93,9 @@ def main(argv=None):
             continue
         start, count = S.shard_range(a.codewords, world, rank)
         t0 = time.time()
-        cnt = run_point(pipe, codec, a.mod, e, count, a.batch, S.shard_seed(a.seed, rank, pi), device)
+        cnt = run_point(pipe, codec, a.mod, e, start, count, a.batch, S.point_seed(a.seed, pi), device)
+        if world > 1 and a.dist_backend != "nccl":
+            cnt = cnt.cpu()
         S.reduce_counters(cnt, dist if world > 1 else None)
         torch.cuda.synchronize()
         be, fe, ncw = (int(x) for x in cnt.tolist())

@@ -15,6 +15,7 @@
 
 #include "tdec.h"
 #include "tdec_kernels.hip"
+#include "tdec_workload.hip"
 
 using namespace tdec;
 
@@ -784,11 +785,87 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     return mark_used(h, st);
 }
 
+}  // extern "C"
+
+// Workload arguments common to the staged encoder kernel's uses.
+static WorkloadArgs workload_args(const tdec_t *h, int B) {
+    WorkloadArgs a{};
+    a.B = B;
+    a.N = h->N;
+    a.period = h->period;
+    a.n_out = h->enc_len;
+    std::memcpy(a.punct, h->punct, 16);
+    std::memcpy(a.circ, h->circ, sizeof a.circ);
+    a.perm = h->d_perm;
+    return a;
+}
+static bool staged_encoder_ok(const tdec_t *h) { return h->N % 4 == 0 && h->N <= ENC_MAX_N; }
+
+extern "C" {
+
+int tdec_workload_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const float *cons_iq, int M, int bps,
+                      double sigma, float *d_syms, uint8_t *d_info, void *stream) {
+    if (!h || B < 0 || cw0 < 0) return fail(TDEC_EINVAL, "bad workload arguments");
+    if (B == 0) return 0;
+    if (!cons_iq || !d_syms || bps < 1 || bps > 8 || M < 1 || M > (1 << bps) || !(sigma >= 0.0))
+        return fail(TDEC_EINVAL, "bad workload arguments");
+    if (!staged_encoder_ok(h)) return fail(TDEC_EINVAL, "workload generation needs N % 4 == 0 and N <= 1024");
+    Guard g(h->device);
+    WorkloadArgs a = workload_args(h, B);
+    a.bps = bps;
+    a.M = M;
+    a.S = (int)((h->enc_len + bps - 1) / bps);
+    a.cw0 = (uint64_t)cw0;
+    a.seed = seed;
+    a.sigma = (float)sigma;
+    for (int m = 0; m < M; ++m) a.cons[m] = make_float2(cons_iq[2 * m], cons_iq[2 * m + 1]);
+    a.info_out = d_info;
+    a.syms = reinterpret_cast<float2 *>(d_syms);
+    hipLaunchKernelGGL(k_workload, dim3((unsigned)n_tiles_of(B)), dim3(64), 0, (hipStream_t)stream, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdec_info_bits_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, uint8_t *d_info, void *stream) {
+    if (!h || B < 0 || cw0 < 0) return fail(TDEC_EINVAL, "bad info-bits arguments");
+    if (B == 0) return 0;
+    if (!d_info) return fail(TDEC_EINVAL, "bad info-bits arguments");
+    if (!staged_encoder_ok(h)) return fail(TDEC_EINVAL, "workload generation needs N % 4 == 0 and N <= 1024");
+    Guard g(h->device);
+    WorkloadArgs a = workload_args(h, B);
+    a.cw0 = (uint64_t)cw0;
+    a.seed = seed;
+    a.info_out = d_info;
+    hipLaunchKernelGGL(k_workload, dim3((unsigned)n_tiles_of(B)), dim3(64), 0, (hipStream_t)stream, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const int32_t *d_bits, int32_t *d_errs,
+                          void *stream) {
+    if (!h || B < 0 || cw0 < 0) return fail(TDEC_EINVAL, "bad count-errors arguments");
+    if (B == 0) return 0;
+    if (!d_bits || !d_errs) return fail(TDEC_EINVAL, "bad count-errors arguments");
+    Guard g(h->device);
+    hipLaunchKernelGGL(k_count_errors, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, B, h->N, (uint64_t)cw0,
+                       seed, d_bits, d_errs);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream) {
     if (!h || B < 0) return fail(TDEC_EINVAL, "bad encode arguments");
     if (B == 0) return 0;
     if (!d_bits || !d_coded) return fail(TDEC_EINVAL, "bad encode arguments");
     Guard g(h->device);
+    if (staged_encoder_ok(h)) {   // coalesced LDS-staged encoder (tdec_workload.hip)
+        WorkloadArgs w = workload_args(h, B);
+        w.bits_in = d_bits;
+        w.coded_out = d_coded;
+        hipLaunchKernelGGL(k_workload, dim3((unsigned)n_tiles_of(B)), dim3(64), 0, (hipStream_t)stream, w);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     EncodeArgs a{};
     a.B = B;
     a.N = h->N;

@@ -5,7 +5,9 @@ ranges, one per rank (one process per GPU, torch.distributed over RCCL on
 the box, gloo in the CPU tests).  Each rank generates its own inputs from a
 counter-based seed, decodes them with no data-path collective, and only the
 three integer error counters (bit errors, frame errors, codewords) are summed
-at the end -- a few bytes of all-reduce.
+at the end -- a few bytes of all-reduce.  The device generator is counted by
+the global codeword index (workload.make_symbols), so a codeword's data does
+not depend on which rank or batch generates it.
 """
 from __future__ import annotations
 
@@ -25,6 +27,13 @@ def shard_range(total, world, rank):
 def shard_seed(base_seed, rank, point=0):
     """Reproducible per-(shard, sweep point) seed: base + 1_000_003*rank + 7919*point."""
     return int(base_seed) + SEED_STRIDE * int(rank) + 7919 * int(point)
+
+
+def point_seed(base_seed, point=0):
+    """Generator key of a sweep point.  With the counter-based generator the
+    codeword's global index is the counter, so the key needs no rank term:
+    every rank of every world size sees the same stream for codeword g."""
+    return int(base_seed) + 7919 * int(point)
 
 
 def batches(count, batch):

@@ -1,7 +1,8 @@
-"""Device-side synthetic workloads: random info bits ->
-batched device encoder (encode, dvb_rcs2_turbo.py:404-462) -> labelled Gray
-constellation (the reference mappers) -> complex AWGN.  Everything stays in
-HBM; nothing here is timed by bench.py."""
+"""Device-side synthetic workloads: counter-based (Philox)
+info bits -> batched device encoder (encode, dvb_rcs2_turbo.py:404-462) ->
+labelled Gray constellation (the reference mappers) -> complex AWGN, and the
+per-codeword error counters of a BER point.  Everything stays in HBM; nothing
+here is timed by bench.py."""
 from __future__ import annotations
 
 import numpy as np
@@ -16,33 +17,56 @@ def noise_n0(constellation, rate, bps, ebn0_db):
     return es / (rate * bps * 10 ** (ebn0_db / 10.0))
 
 
-def make_symbols(codec, B, mod, ebn0_db, seed, device):
-    """(info uint8 [B, 2N], received symbols complex64 [B, S], N0) on `device`.
+def make_symbols(codec, B, mod, ebn0_db, seed, device, cw0=0, want_info=True):
+    """(info uint8 [B, 2N] or None, received symbols complex64 [B, S], N0) on `device`.
 
-    The coded stream of each codeword is zero-padded to whole symbols as the
-    reference mappers pad (test_sdr_with_coding.py:45-86)."""
+    One launch of the counter-based generator (tdec_workload_dev): Philox info
+    bits of GLOBAL codewords cw0 .. cw0+B-1 -> the LDS-staged encoder ->
+    labelled Gray constellation (bps coded bits per label, MSB first, the last
+    symbol zero-padded as the reference mappers pad, test_sdr_with_coding.py:45-86)
+    -> complex AWGN with per-dimension variance N0/2.  Codeword g's data is the
+    same whichever batch or rank generates it."""
     import torch
+    from . import _native as _n
     bps = D.MODULATIONS[mod]["bps"]
     cons = D.constellation(mod)
     rate = codec.k_info / codec.n_coded
-    g = torch.Generator(device=device)
-    g.manual_seed(int(seed))
-    info = torch.randint(0, 2, (B, codec.k_info), generator=g, device=device, dtype=torch.uint8)
-    coded = codec.encode_device(info)
-    n = coded.shape[1]
-    S = -(-n // bps)
-    if S * bps > n:
-        coded = torch.nn.functional.pad(coded, (0, S * bps - n))
-    w = 1 << torch.arange(bps - 1, -1, -1, device=device, dtype=torch.int32)
-    labels = (coded.view(B, S, bps).to(torch.int32) * w).sum(-1)
-    del coded
-    table = torch.from_numpy(np.ascontiguousarray(cons.astype(np.complex64))).to(device)
-    x = table[labels]
-    del labels
+    h = codec.handle
+    S = -(-h.enc_len // bps)
     n0 = noise_n0(cons, rate, bps, ebn0_db)
-    noise = torch.randn((B, S, 2), generator=g, device=device, dtype=torch.float32) * float(np.sqrt(n0 / 2))
-    y = (x + torch.view_as_complex(noise)).contiguous()
-    return info, y, n0
+    table = np.ascontiguousarray(cons.astype(np.complex64)).view(np.float32)
+    syms = torch.empty((B, S), dtype=torch.complex64, device=device)
+    info = torch.empty((B, codec.k_info), dtype=torch.uint8, device=device) if want_info else None
+    h.call("tdec_workload_dev", int(B), int(cw0), int(seed) & 0xFFFFFFFFFFFFFFFF, _n.ptr(table), len(cons), bps,
+           float(np.sqrt(n0 / 2)), _n.ptr(syms), _n.ptr(info), codec._stream(None))
+    return info, syms, n0
+
+
+def info_bits(codec, B, seed, device, cw0=0):
+    """The info bits make_symbols encodes, uint8 [B, 2N]."""
+    import torch
+    info = torch.empty((B, codec.k_info), dtype=torch.uint8, device=device)
+    codec.handle.call("tdec_info_bits_dev", int(B), int(cw0), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                      _ptr(info), codec._stream(None))
+    return info
+
+
+def count_errors(codec, bits, seed, cw0=0):
+    """Bit errors per codeword (int32 [B]) of decoded rows against the
+    counter-based info bits of global codewords cw0 .. cw0+B-1."""
+    import torch
+    B = bits.shape[0]
+    if bits.dtype != torch.int32 or not bits.is_contiguous() or tuple(bits.shape) != (B, codec.k_info):
+        raise ValueError("bits must be a contiguous int32 [B, 2N] tensor")
+    errs = torch.empty(B, dtype=torch.int32, device=bits.device)
+    codec.handle.call("tdec_count_errors_dev", int(B), int(cw0), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(bits),
+                      _ptr(errs), codec._stream(None))
+    return errs
+
+
+def _ptr(t):
+    from . import _native as _n
+    return _n.ptr(t)
 
 
 class DevicePipeline:
@@ -65,7 +89,8 @@ class DevicePipeline:
         self.codec.demap_planes_device(syms, self.cons, self.bps, nve, self.planes, div_f32=div32, stream=stream)
         if events is not None:
             events[0].record(stream)
-        self.codec.decode_planes_device(self.planes, syms.shape[0], self.bits, stream=stream)
+        bits = self.bits[:syms.shape[0]]          # the first rows: a contiguous view
+        self.codec.decode_planes_device(self.planes, syms.shape[0], bits, stream=stream)
         if events is not None:
             events[1].record(stream)
-        return self.bits
+        return bits

@@ -7,7 +7,7 @@ WRITE_SIZE come from separate --pmc passes, are in KiB, and on gfx950 FETCH_SIZE
 reads exactly half the bytes of a wide coalesced streaming read, so
 hbm_bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 
-usage: tools/prof_summary.py gpurun_out/r01 profiles/r01 [batch]
+usage: tools/prof_summary.py gpurun_out/r01 profiles/r01 [batch] [workload string: stamp profiles/traffic.json]
 """
 import collections
 import csv
@@ -50,7 +50,11 @@ def pmc(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(src, dst, batch=1 << 20):
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FETCH_FACTOR = 2.0   # MI355X_MICROARCH.md: FETCH_SIZE counts half of a wide streaming read (re-checked: r02_fetch_cal)
+
+
+def main(src, dst, batch=1 << 20, workload=None):
     batch = int(batch)
     out = {"source": src, "batch_codewords": batch, "kernels": {}}
     trace = full_size(list(csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))), span)
@@ -69,7 +73,7 @@ def main(src, dst, batch=1 << 20):
         c = {cn: v for (kk, cn), v in counters.items() if kk == k}
         d["counters"] = c
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            rd = 2 * c["FETCH_SIZE"] * 1024
+            rd = FETCH_FACTOR * c["FETCH_SIZE"] * 1024
             wr = c["WRITE_SIZE"] * 1024
             d["hbm_read_bytes"] = rd
             d["hbm_write_bytes"] = wr
@@ -91,6 +95,28 @@ def main(src, dst, batch=1 << 20):
             # VALU issue-busy share: wave-instructions x 2 cycles (SIMD-32) / (1024 SIMDs x cycles)
             d["valu_busy_est"] = c.get("SQ_INSTS_VALU", 0) * 2 / (1024 * clk * d["avg_ms"] * 1e-3)
     json.dump(out, open(dst + "_summary.json", "w"), indent=1)
+    if workload:   # stamp profiles/traffic.json with the library this run loaded
+        import hashlib
+        lib = os.path.join(ROOT, "modulations_amd", "lib", "libtdec.so")
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        tr = json.load(open(tf)) if os.path.exists(tf) else {}
+        for k in ("k_turbo_decode", "k_turbo_decode_logmap"):
+            d = out["kernels"].get(k)
+            if not d or "hbm_bytes_per_codeword" not in d:
+                continue
+            ent = tr.get(k, {})
+            if not isinstance(ent, dict) or "workload" in ent:   # round-1 flat format
+                ent = {}
+            ent[workload] = {"hbm_bytes_per_codeword": d["hbm_bytes_per_codeword"],
+                             "hbm_read_bytes_per_codeword": d["hbm_read_bytes"] / batch,
+                             "hbm_write_bytes_per_codeword": d["hbm_write_bytes"] / batch,
+                             "avg_ms": d["avg_ms"], "lib_sha256": sha, "source": dst + "_summary.json",
+                             "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (KiB); "
+                                       f"FETCH_SIZE x {FETCH_FACTOR} (gfx950 read calibration, "
+                                       "profiles/r02_fetch_cal.txt); per launch / codewords per launch"}
+            tr[k] = ent
+        json.dump(tr, open(tf, "w"), indent=1)
     with open(dst + "_summary.md", "w") as f:
         f.write(f"# rocprofv3 summary ({src}), batch = {batch} codewords\n\n")
         f.write("| kernel | calls | avg ms | HBM GB/launch | HBM GB/s | B/codeword | L2 hit | VALU busy (est) | wait_any | wait_inst | clock GHz |\n")

@@ -13,6 +13,8 @@ restates the reference module's table code:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 # Interleaver parameters (reference :12-17), keyed by N in couples.
@@ -92,12 +94,24 @@ def inverse_interleaver(perm, mode='stable'):
     mode='stable'  -- ``np.argsort(perm, kind='stable')``: the build's canonical,
                       host-independent pin (default).
     mode='numpy'   -- exactly the reference expression evaluated on THIS host.
+    mode='numpy-avx512' -- the reference expression as numpy 2.2 evaluates it on
+                      an AVX-512 host (the survey's container): a pinned table
+                      (data/inv_perm_numpy_avx512.npz, the ``inv_default_*``
+                      golden arrays), so the reference's result on that host is
+                      reproduced on any host.
     """
     perm = np.asarray(perm)
     if mode == 'stable':
         return np.argsort(perm, kind='stable').astype(np.int32)
     if mode == 'numpy':
         return np.argsort(perm).astype(np.int32)
+    if mode == 'numpy-avx512':
+        n = len(perm)
+        if n not in INTERLEAVER_PARAMS or not np.array_equal(perm, interleaver(n)):
+            raise ValueError("'numpy-avx512' is pinned for the reference interleaver of the table block sizes only")
+        tab = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "inv_perm_numpy_avx512.npz"),
+                      allow_pickle=False)
+        return tab[f"inv_{n}"].astype(np.int32)
     raise ValueError(f"unknown inverse-interleaver mode {mode!r}")
 
 

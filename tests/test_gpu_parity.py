@@ -101,6 +101,26 @@ def test_decode_golden(G_decode):
         assert np.array_equal(c.decode(G_decode[f"llr_{key}"][0]), G_decode[f"bits_{key}"][0])
 
 
+def test_decode_reference_host_default_fixtures(G_decode):
+    """The *_default fixtures were decoded by the reference with its own
+    inv_perm = np.argsort(perm) on the survey's AVX-512 host.  The drop-in
+    reproduces them with the one-line switch inv_perm='numpy-avx512' (and with
+    inv_perm='numpy' wherever this host's numpy sorts the same way)."""
+    from modulations_amd import tables as T
+    keys = sorted(k[4:] for k in G_decode.files if k.startswith("llr_") and k.endswith("_default"))
+    assert keys
+    for key in keys:
+        n, r1, r2, _ = key.split("_")
+        c = M.DVBRCS2_Turbo(int(n), f"{r1}/{r2}", inv_perm="numpy-avx512")
+        assert np.array_equal(c.inv_perm, G_decode[f"inv_{key}"])
+        bits, lf = c.decode_batch(G_decode[f"llr_{key}"], return_lfinal=True)
+        assert np.array_equal(bits, G_decode[f"bits_{key}"]), key
+        assert np.array_equal(lf, G_decode[f"lfinal_{key}"]), key
+        if np.array_equal(T.inverse_interleaver(c.perm, "numpy"), G_decode[f"inv_{key}"]):
+            c2 = M.DVBRCS2_Turbo(int(n), f"{r1}/{r2}", inv_perm="numpy")
+            assert np.array_equal(c2.decode_batch(G_decode[f"llr_{key}"]), G_decode[f"bits_{key}"]), key
+
+
 @pytest.mark.parametrize("n", [48, 212, 752])
 def test_noise_free_kat(G_decode, n):
     """21 / 83 / 355 errors from the broken interleaver."""

@@ -94,3 +94,17 @@ def test_legacy_codec_shim():
         M.DVB_RCS2_TurboCodec(block_length=212, code_rate='2/5')    # in the harness menu, not in the tables
     with pytest.raises(ValueError):
         M.DVB_RCS2_TurboCodec(block_length=228, code_rate='1/3')
+
+
+def test_numpy_avx512_inverse_is_a_pinned_argsort(G_tables):
+    """inv_perm='numpy-avx512' reproduces the reference's np.argsort(perm) as the
+    survey's AVX-512 numpy 2.2 host evaluated it, on any host."""
+    from modulations_amd import tables as T
+    for n in (48, 64, 212, 220, 424, 752, 848):
+        perm = T.interleaver(n)
+        inv = T.inverse_interleaver(perm, "numpy-avx512")
+        assert np.array_equal(inv, G_tables[f"inv_default_{n}"])
+        assert sorted(inv.tolist()) == list(range(n))            # a permutation
+        assert np.all(np.diff(perm[inv]) >= 0)                   # that sorts perm
+    with pytest.raises(ValueError):
+        T.inverse_interleaver(T.valid_interleaver(48), "numpy-avx512")

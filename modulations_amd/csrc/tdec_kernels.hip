@@ -517,6 +517,19 @@ __device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float
     return __all(eq);
 }
 
+// This lane's vector equals the stored one (IEEE ==).
+template <bool ALPHA>
+__device__ __forceinline__ bool lane_equal(const float (&x)[NS], const float4 *c, unsigned cs, unsigned base, int lane) {
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = at(c, (base + q) * cs + lane);
+        eq = eq && x[vec_elem<ALPHA>(q, 0)] == v.x && x[vec_elem<ALPHA>(q, 1)] == v.y &&
+             x[vec_elem<ALPHA>(q, 2)] == v.z && x[vec_elem<ALPHA>(q, 3)] == v.w;
+    }
+    return eq;
+}
+
 template <bool ALPHA>
 __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base, int lane, const float (&x)[NS]) {
 #pragma unroll
@@ -639,25 +652,37 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         for (int j = 0; j < W; ++j)
             if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
     }
-    // F2 until merged (a = alpha1[N] = alpha2[0])
+    // F2 until merged (a = alpha1[N] = alpha2[0]).  Per lane: once alpha2 ==
+    // alpha1 at a checkpoint, every later checkpoint already holds alpha2, so
+    // the lane stops loading and storing (masked lanes move no bytes); the
+    // wave runs until every lane has merged.
+#ifndef TDEC_LANE_MERGE
+#define TDEC_LANE_MERGE 1
+#endif
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
+    bool merged = false;
     for (int k0 = 0; k0 < N; k0 += W) {
-        if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
-        float g[W][8];
+        if (TDEC_LANE_MERGE) {
+            if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / W) * 4, lane);
+            if (__all(merged)) break;
+        } else if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
+        if (!merged) {
+            float g[W][8];
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            double iA, iB;
-            in.gamma(raw[j], g[j], iA, iB);
+            for (int j = 0; j < W; ++j) {
+                double iA, iB;
+                in.gamma(raw[j], g[j], iA, iB);
+            }
+            if (k0 + W < N) {
+#pragma unroll
+                for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
+            }
+            store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
-        if (k0 + W < N) {
-#pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
-        }
-        store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
-#pragma unroll
-        for (int j = 0; j < W; ++j)
-            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
     }
     // B1 fused with the provisional extrinsic
     float b[NS];
@@ -670,13 +695,23 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
         back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
     }
-    // B2 until merged (b = beta1[0] = beta2[N])
+    // B2 until merged (b = beta1[0] = beta2[N]); per lane as F2: below its
+    // merge point a lane's provisional extrinsics are exact, it stops there
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+    merged = false;
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;
-        if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
-        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+        if (TDEC_LANE_MERGE) {
+            if (r % RSTEP == 0 && r < RING * RSTEP) {
+                if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP * 4, lane);
+                if (__all(merged)) break;
+            }
+            if (!merged) back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+        } else {
+            if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
+            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+        }
     }
 }
 
@@ -902,9 +937,13 @@ struct DecodeArgs {
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
+#ifndef TDEC_EPI_LDS
+#define TDEC_EPI_LDS 1
+#endif
 template <int ALGO, bool RAG>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
-                                                   const int *__restrict__ inv, float4 *lv, double2 *ll) {
+                                                   const int *__restrict__ inv, float4 *lv, double2 *ll,
+                                                   uint32_t *epi) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
@@ -930,6 +969,53 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
+#if TDEC_EPI_LDS
+        // Bits of 32 couples per lane are packed into two LDS words, then the wave
+        // writes the 64 rows chunk by chunk in row order (16-B int4 stores, each
+        // wave store one contiguous 1 KiB run) instead of one 8-B store per lane
+        // per couple 6 KB apart.
+        uint32_t *hb = epi + (threadIdx.x >> 6) * 2 * WAVE;
+        const long nb = 2L * N;
+        for (int kc = 0; kc < N; kc += 32) {
+            uint32_t w0 = 0, w1 = 0;
+            double *lo = (p.lfinal && cw < p.B) ? p.lfinal + cw * nb : nullptr;
+            const int kn = min(32, N - kc);
+            for (int kk = 0; kk < kn; ++kk) {
+                const int k = kc + kk;
+                const float4 x = at(X, k * WAVE + lane);
+                const double2 la = at(Le2, inv[k] * rs + lane);
+                const double2 le = at(Le1, k * rs + lane);
+                const double fa = ((double)x.x + la.x) + le.x;
+                const double fb = ((double)x.y + la.y) + le.y;
+                const uint32_t two = (fa < 0.0 ? 1u : 0u) | (fb < 0.0 ? 2u : 0u);
+                if (kk < 16) w0 |= two << (2 * kk);
+                else w1 |= two << (2 * (kk - 16));
+                if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
+            }
+            hb[lane] = w0;
+            hb[WAVE + lane] = w1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // 64 rows x 2*kn int32 of this chunk: item t = (row, 4-bit piece)
+            const int per = (2 * kn + 3) / 4;
+            for (int t = lane; t < WAVE * per; t += WAVE) {
+                const int l = t / per, pc = t - l * per;
+                const long row = (long)tile * WAVE + l;
+                if (row >= p.B) continue;
+                const uint32_t w = hb[(pc >> 3) * WAVE + l] >> (4 * (pc & 7));
+                const int j = 4 * pc;                          // first int32 of the piece within the chunk
+                int32_t *dst = p.bits + row * nb + 2L * kc + j;
+                if (j + 4 <= 2 * kn && (nb & 3) == 0)
+                    *reinterpret_cast<int4 *>(dst) = make_int4(w & 1, (w >> 1) & 1, (w >> 2) & 1, (w >> 3) & 1);
+                else
+                    for (int e = 0; e < 4 && j + e < 2 * kn; ++e) dst[e] = (w >> e) & 1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#else
         if (cw < p.B) {
             int32_t *bo = p.bits + cw * 2 * N;
             double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
@@ -943,6 +1029,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                 if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
             }
         }
+#endif
     }
 }
 
@@ -958,7 +1045,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_W
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
     __shared__ float4 lv[LDS_STAGE];
     __shared__ double2 ll[LDS_STAGE];
-    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll);
+    __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll, epi);
 }
 #ifndef TDEC_LM_WPE
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
@@ -966,7 +1054,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_W
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
-    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr);
+    __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr, epi);
 }
 
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).

@@ -349,7 +349,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     h->max_waves = std::max(1, blocks_per_cu) * n_cu * WAVES_PER_BLOCK;
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
-    const long row_units = std::max<long>(N, 4L * ((N + WIN - 1) / WIN + RING));
+    const long row_units = std::max<long>(N, 4L * ((N + WIN_MIN - 1) / WIN_MIN + RING));
     const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
     h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
     // experiment knob: run the persistent decoder on a percentage of the resident waves
@@ -396,7 +396,7 @@ static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 
 // Per-wave workspace strides (elements).
 static long ws_stride_of(const tdec_t *h) { return 3L * h->N * WAVE; }
-static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN - 1) / WIN + RING) * 4 * WAVE; }
+static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) / WIN_MIN + RING) * 4 * WAVE; }
 
 // Time one single-iteration decode of waves*64 codewords of constant LLRs on a
 // candidate workspace (the placement probe below).

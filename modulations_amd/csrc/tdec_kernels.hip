@@ -80,8 +80,9 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
 }
 
 // ---- max / max* ---------------------------------------------------------------
-// log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) with the
-// historic 37 cut-off.  The correction is defined as this exact sequence of f32
+// log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) (the
+// historic _jacobian_log-22 cut it off at 37; here the exponential itself
+// underflows to 0 past 104).  The correction is defined as this exact sequence of f32
 // IEEE operations (explicit fused multiply-adds, no division), the same
 // sequence the oracle restates, so log-MAP is bit-exact too.  In the
 // recursions each state's two parallel branches are combined first,
@@ -89,18 +90,22 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
 // or beta step costs 8 shared pair max* + 16, not 48; the extrinsic keeps one
 // max* per branch.  Result: within 4e-6 of log-MAP with exact f64 Jacobian
 // logarithms (tests/test_oracle_golden.py).
-__device__ __forceinline__ float jac_corr(float d) {
+__device__ __forceinline__ float exp_neg(float d) {           /* exp(-d), 0 <= d <= 150 */
     const float x = d * 0x1.715476p+0f;                     /* d * log2(e) */
-    const int n = (int)x;
-    const float f = x - (float)n;                             /* exact, in [0, 1) */
+    // n = trunc(x) and f = x - n (exact, in [0, 1)) as v_cvt_i32_f32 of -x and
+    // v_fract_f32 of x: the oracle's (int)x / x - (float)n, two instructions fewer
+    const int nn = (int)(-x);                                 /* -n */
+    const float f = __builtin_amdgcn_fractf(x);
     float p = -0x1.f0ca8p-11f;                                /* 2^-f */
     p = fmaf(p, f, 0x1.2dd26cp-7f);
     p = fmaf(p, f, -0x1.c503aep-5f);
     p = fmaf(p, f, 0x1.ebe33ap-3f);
     p = fmaf(p, f, -0x1.62e3aap-1f);
     p = fmaf(p, f, 0x1.fffffep-1f);
-    const float e = ldexpf(p, -n);                            /* exp(-d) */
-    float q = -0x1.18f998p-7f;                                /* log1p(e) / e, e in (0, 1] */
+    return ldexpf(p, nn);
+}
+__device__ __forceinline__ float log1p_01(float e) {          /* log1p(e), e in [0, 1] */
+    float q = -0x1.18f998p-7f;                                /* log1p(e) / e */
     q = fmaf(q, e, 0x1.6a33e2p-5f);
     q = fmaf(q, e, -0x1.b9c4c8p-4f);
     q = fmaf(q, e, 0x1.6ba9f2p-3f);
@@ -110,12 +115,34 @@ __device__ __forceinline__ float jac_corr(float d) {
     q = fmaf(q, e, 0x1.fffffap-1f);
     return q * e;
 }
+__device__ __forceinline__ float jac_corr(float d) { return log1p_01(exp_neg(d)); }
+// log(S) for a positive normal S: S = 2^k (1 + u), u in [0, 1) exact, log = k ln2 + log1p(u)
+__device__ __forceinline__ float log_pos(float S) {
+    const int bits = __float_as_int(S);
+    const int k = (bits >> 23) - 127;
+    const float u = __int_as_float((bits & 0x7FFFFF) | 0x3F800000) - 1.0f;
+    return fmaf((float)k, 0x1.62e43p-1f, log1p_01(u));
+}
+// log-MAP marginal over the 16 states (the extrinsic's app[inp], build-defined):
+// M = max_s t[s] (maxNum), S = sum_s exp(-(M - t[s])) in state order with the
+// difference clamped to 150, app = M + log(S).  The log-sum-exp of 16 terms
+// costs 16 exponentials and one logarithm instead of a chain of 15 Jacobian
+// logarithms (15 of each), and is the exact f64 reference's definition
+// (np.logaddexp.reduce over the states) up to f32 rounding.
+__device__ __forceinline__ float lse16(const float (&t)[NS]) {
+    float m = t[0];
+#pragma unroll
+    for (int s = 1; s < NS; ++s) m = fmaxf(m, t[s]);
+    float S = 0.0f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) S += exp_neg(fminf(m - t[s], 150.0f));
+    return m + log_pos(S);
+}
 
+// max*(a, b) = maxNum(a, b) + log1p(exp(-min(|a - b|, 150))): the correction is
+// exactly 0 from |a - b| > 104 on (exp underflows), a NaN operand is dropped.
 __device__ __forceinline__ float jac(float a, float b) {
-    const float m = a > b ? a : b;
-    const float d = fabsf(a - b);
-    const float c = jac_corr(d <= 37.0f ? d : 0.0f);   // branch-free; operand kept in range
-    return (d <= 37.0f) ? m + c : m;                     // NaN d and d > 37 keep m
+    return fmaxf(a, b) + jac_corr(fminf(fabsf(a - b), 150.0f));
 }
 
 template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {
@@ -123,14 +150,13 @@ template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {
     else return jac(m, t);
 }
 
-// acc(NEG, t): the first step of every running max*.  |NEG - t| > 37 for any
-// finite metric, so the wave skips the correction unless some lane needs it
-// (same value either way).
+// acc(NEG, t): the first step of every running max*.  |NEG - t| >= 150 for any
+// metric above -1e9 + 150, where the correction is exactly 0, so the wave
+// skips it unless some lane needs it (the same bits either way).
 template <int ALGO> __device__ __forceinline__ float acc_first(float t) {
     if constexpr (ALGO == 0) return fmaxf(NEG, t);
     else {
-        const float d = fabsf(NEG - t);
-        if (__all(!(d <= 37.0f))) return NEG > t ? NEG : t;
+        if (__all(fabsf(NEG - t) >= 150.0f)) return fmaxf(NEG, t) + 0.0f;
         return jac(NEG, t);
     }
 }
@@ -275,6 +301,9 @@ template <int E> __device__ __forceinline__ f2 pk_add_bcast(f2 t, f2 y) {
     return r;
 }
 
+#ifndef TDEC_LM_LSE
+#define TDEC_LM_LSE 1
+#endif
 template <int ALGO>
 __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)[8], const float (&b1)[NS], double inA,
                                           double inB, double sf, double &leA, double &leB) {
@@ -305,6 +334,15 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
             }
         }
     } else {
+#if TDEC_LM_LSE
+#pragma unroll
+        for (int inp = 0; inp < 4; ++inp) {
+            float t[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) t[s] = (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)];
+            app[inp] = lse16(t);
+        }
+#else
 #pragma unroll
         for (int inp = 0; inp < 4; ++inp) app[inp] = acc_first<ALGO>((a[0] + gam(g, 0, inp)) + b1[t_next(0, inp)]);
 #pragma unroll
@@ -312,6 +350,7 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
 #pragma unroll
             for (int inp = 0; inp < 4; ++inp)
                 app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
+#endif
     }
     const float pA0 = star<ALGO>(app[0], app[1]), pA1 = star<ALGO>(app[2], app[3]);
     const float pB0 = star<ALGO>(app[0], app[2]), pB1 = star<ALGO>(app[1], app[3]);
@@ -623,12 +662,14 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 //       values are exact (a pass that has not merged by then runs to the end).
 // ck: alpha checkpoints [ceil(N/W)][4][64] float4; ring: beta1 [RING][4][64].
 // Any N >= 1: only the top window can be short, every guard is wave-uniform.
-constexpr int RING = 16, RSTEP = 4;   // beta1 kept over the top 256 steps (merge: median 40, max 122)
+constexpr int RING = 16;   // beta1 kept at RING window starts 16 steps apart: the top 256 steps (merge: median 40, max 122)
+__host__ __device__ constexpr int rstep_of(int w) { return w >= 16 ? 1 : 16 / w; }
 
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane,
                      double sf) {
     const int top = RAG ? ((N - 1) / W) * W : N - W;   // start of the (possibly short) top window
+    constexpr int RSTEP = rstep_of(W);
     Raw raw[W];
     float a[NS];
 #pragma unroll
@@ -850,23 +891,29 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
     // F2 until merged with F1 at a checkpoint
 #pragma unroll
     for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
+    bool merged = false;   // per lane, as siso<>
     for (int k0 = 0; k0 < N; k0 += G) {
         const bool at_ck = (k0 & (CK - 1)) == 0;
-        if (at_ck && wave_all_equal<true>(a, ck, cs, (k0 / CK) * 4, lane)) break;
-        float g[G][8];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            double iA, iB;
-            in.gamma(raw[j], g[j], iA, iB);
+        if (at_ck) {
+            if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / CK) * 4, lane);
+            if (__all(merged)) break;
         }
-        if (k0 + G < N) {
+        if (!merged) {
+            float g[G][8];
 #pragma unroll
-            for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(k0 + G + j, N - 1) : k0 + G + j);
+            for (int j = 0; j < G; ++j) {
+                double iA, iB;
+                in.gamma(raw[j], g[j], iA, iB);
+            }
+            if (k0 + G < N) {
+#pragma unroll
+                for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(k0 + G + j, N - 1) : k0 + G + j);
+            }
+            if (at_ck) store_vec<true>(ck, cs, (k0 / CK) * 4, lane, a);
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
-        if (at_ck) store_vec<true>(ck, cs, (k0 / CK) * 4, lane, a);
-#pragma unroll
-        for (int j = 0; j < G; ++j)
-            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
     }
     // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
     float b[NS];
@@ -879,12 +926,16 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
             raw[j] = in.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
             in.stage(RAG ? min(top + j, N - 1) : top + j, lb, j);
         }
+        merged = false;
         for (int k0 = top; k0 >= 0; k0 -= CK) {
             const int r = (top - k0) / CK;
             const bool keep = r % RSTEP8 == 0 && r < RING * RSTEP8;
             if (pass == 0 && keep) store_vec<false>(ring, cs, r / RSTEP8 * 4, lane, b);   // beta1 entering
-            if (pass == 1 && keep && wave_all_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane)) break;
-            back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, lb, b, ck, cs, lane, sf);
+            if (pass == 1 && keep) {
+                if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane);
+                if (__all(merged)) break;
+            }
+            if (!merged) back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, lb, b, ck, cs, lane, sf);
         }
     }
 }
@@ -895,7 +946,7 @@ constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 #ifndef TDEC_WIN
 #define TDEC_WIN 4
 #endif
-constexpr int WIN = TDEC_WIN;            // log-MAP alpha checkpoint interval; the workspace is sized for it
+constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval of the row SISO (k_siso_batch)
 #ifndef TDEC_WIN_ML
 #define TDEC_WIN_ML 4
 #endif
@@ -906,7 +957,13 @@ constexpr int WIN = TDEC_WIN;            // log-MAP alpha checkpoint interval; t
 // expose latency that two waves per SIMD do not hide.  Kept as an A/B variant
 // (python -m modulations_amd.build --variant ml8 TDEC_WIN_ML=8).
 constexpr int WIN_ML = TDEC_WIN_ML;
-__host__ __device__ constexpr int win_of(int algo) { return algo ? WIN : WIN_ML; }
+#ifndef TDEC_WIN_LM
+#define TDEC_WIN_LM 2
+#endif
+constexpr int WIN_LM = TDEC_WIN_LM;      // log-MAP turbo decoder's checkpoint interval
+__host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_ML; }
+// the workspace's checkpoint array is sized for the densest interval in use
+constexpr int WIN_MIN = WIN < WIN_ML ? (WIN < WIN_LM ? WIN : WIN_LM) : (WIN_ML < WIN_LM ? WIN_ML : WIN_LM);
 constexpr int LDS_STAGE = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of a block's staging planes
 
 // The SISO of the tile decoder: siso8 for max-log at WIN_ML 8, else siso<> at WIN.
@@ -917,7 +974,7 @@ __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, fl
         const int w = threadIdx.x >> 6;
         siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{lv + w * 4 * WAVE, ll + w * 4 * WAVE, lane});
     } else {
-        siso<ALGO, (ALGO ? WIN : WIN_ML), RAG>(in, out, N, ck, ring, cs, lane, sf);
+        siso<ALGO, (ALGO ? WIN_LM : WIN_ML), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
 }
 
@@ -952,7 +1009,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
     const unsigned rs = (unsigned)p.n_waves * WAVE;
     double2 *P1 = p.ws + (long)wave * WAVE, *Le2 = P1 + (long)N * rs, *Le1 = Le2 + (long)N * rs;
-    const int nw = (N + WIN - 1) / WIN;
+    const int nw = (N + WIN_MIN - 1) / WIN_MIN;
     float4 *ck = p.ck + (long)wave * WAVE;
     float4 *ring = ck + (long)nw * 4 * rs;
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {

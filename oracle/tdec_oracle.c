@@ -93,15 +93,15 @@ void orc_interleaver(int N, const int32_t *params, int32_t *perm, int32_t *inv_s
 static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
 
 /* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm
- * max(a,b) + log1p(exp(-|a-b|)), with the cut-off (|a-b| > 37 -> max) of the
- * historic _jacobian_log-22.  The correction is DEFINED as the fixed sequence of
+ * max(a,b) + log1p(exp(-|a-b|)) (the historic _jacobian_log-22 cut it off at
+ * |a-b| > 37; here exp itself underflows to 0 past 104).  The correction is DEFINED as the fixed sequence of
  * f32 IEEE operations below -- exp(-d) = 2^-n * 2^-f from x = d*log2(e) (f = x - n
  * exact), a degree-5 polynomial for 2^-f and log1p(e) = e * Q(e) with a degree-7 Q,
  * all as fused multiply-adds
  * (fmaf is correctly rounded everywhere) -- |error| < 2.5e-7 against the real
  * function.  The HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr)
  * restates it bit for bit instead of depending on two different libms. */
-static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
+static inline float exp_neg(float d)   /* exp(-d), 0 <= d <= 150 */
 {
     const float x = d * 0x1.715476p+0f;                     /* d * log2(e) */
     const int n = (int)x;
@@ -112,8 +112,12 @@ static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
     p = fmaf(p, f, 0x1.ebe33ap-3f);
     p = fmaf(p, f, -0x1.62e3aap-1f);
     p = fmaf(p, f, 0x1.fffffep-1f);
-    const float e = ldexpf(p, -n);                            /* exp(-d) */
-    float q = -0x1.18f998p-7f;                                /* log1p(e) / e, e in (0, 1] */
+    return ldexpf(p, -n);
+}
+
+static inline float log1p_01(float e)   /* log1p(e), e in [0, 1] */
+{
+    float q = -0x1.18f998p-7f;                                /* log1p(e) / e */
     q = fmaf(q, e, 0x1.6a33e2p-5f);
     q = fmaf(q, e, -0x1.b9c4c8p-4f);
     q = fmaf(q, e, 0x1.6ba9f2p-3f);
@@ -124,12 +128,40 @@ static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 37 */
     return q * e;
 }
 
+static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 150 */
+{
+    return log1p_01(exp_neg(d));
+}
+
+/* log(S) for a positive normal S: S = 2^k (1 + u), u in [0, 1) exact */
+static inline float log_pos(float S)
+{
+    int32_t bits;
+    memcpy(&bits, &S, 4);
+    const int k = (bits >> 23) - 127;
+    const int32_t mb = (bits & 0x7FFFFF) | 0x3F800000;
+    float m;
+    memcpy(&m, &mb, 4);
+    return fmaf((float)k, 0x1.62e43p-1f, log1p_01(m - 1.0f));
+}
+
+/* log-MAP marginal over the 16 states (the extrinsic's app[inp], build-defined):
+ * M = max_s t[s] (maxNum), S = sum over s in state order of exp(-min(M - t[s], 150)),
+ * app = M + log(S).  Kernel: lse16 in tdec_kernels.hip. */
+static inline float lse16(const float *t)
+{
+    float m = t[0];
+    for (int s = 1; s < NS; ++s) m = fmaxf(m, t[s]);
+    float S = 0.0f;
+    for (int s = 0; s < NS; ++s) S += exp_neg(fminf(m - t[s], 150.0f));
+    return m + log_pos(S);
+}
+
+/* max*(a, b) = maxNum(a, b) + log1p(exp(-min(|a - b|, 150))): the correction is
+ * exactly 0 past |a - b| = 104 (exp underflows); a NaN operand is dropped. */
 static inline float jac(float a, float b)
 {
-    float m = a > b ? a : b;
-    float d = fabsf(a - b);
-    if (!(d <= 37.0f)) return m;       /* NaN d or d > 37: plain max */
-    return m + jac_corr(d);
+    return fmaxf(a, b) + jac_corr(fminf(fabsf(a - b), 150.0f));
 }
 
 float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy test */
@@ -228,12 +260,20 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
     /* 4. extrinsic (:232-281) */
     for (int k = 0; k < N; ++k) {
         float app[4] = {(float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL};
-        for (int s = 0; s < NS; ++s)
+        if (algo) {
             for (int inp = 0; inp < 4; ++inp) {
-                int n = nx[s * 4 + inp];
-                float metric = ALP(k, s) + GAM(k, s, inp) + BET(k + 1, n);
-                app[inp] = algo ? jac(app[inp], metric) : maxlog_acc(app[inp], metric);
+                float t[NS];
+                for (int s = 0; s < NS; ++s) t[s] = ALP(k, s) + GAM(k, s, inp) + BET(k + 1, nx[s * 4 + inp]);
+                app[inp] = lse16(t);
             }
+        } else {
+            for (int s = 0; s < NS; ++s)
+                for (int inp = 0; inp < 4; ++inp) {
+                    int n = nx[s * 4 + inp];
+                    float metric = ALP(k, s) + GAM(k, s, inp) + BET(k + 1, n);
+                    app[inp] = maxlog_acc(app[inp], metric);
+                }
+        }
         float pA0 = star(algo, app[0], app[1]);
         float pA1 = star(algo, app[2], app[3]);
         float pB0 = star(algo, app[0], app[2]);

@@ -43,17 +43,18 @@ def main():
     ap.add_argument("--n", type=int, default=752)
     ap.add_argument("--rate", default="1/3")
     ap.add_argument("--algo", type=int, default=0)
+    ap.add_argument("--mod", default="16QAM")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     codec = M.DVBRCS2_Turbo(a.n, a.rate)
     B = a.batch
-    info, syms, n0 = make_symbols(codec, B, "16QAM", 2.0, 99, dev)
+    info, syms, n0 = make_symbols(codec, B, a.mod, 2.0, 99, dev)
     from modulations_amd import demap as D
-    cons = D.constellation("16QAM")
+    cons = D.constellation(a.mod)
     _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
     planes = torch.empty(codec.planes_bytes(B) // 4, dtype=torch.float32, device=dev)
     codec.reserve(B)
-    codec.demap_planes_device(syms, cons, 4, nve, planes, div_f32=div32)
+    codec.demap_planes_device(syms, cons, D.MODULATIONS[a.mod]["bps"], nve, planes, div_f32=div32)
     torch.cuda.synchronize()
     tabs = T.packed_tables(codec.next_state, codec.out_W, codec.out_Y, codec.prev_state, codec.prev_input)
     pm = T.puncture_matrix(codec.punct)

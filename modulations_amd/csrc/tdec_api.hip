@@ -16,6 +16,7 @@
 #include "tdec.h"
 #include "tdec_kernels.hip"
 #include "tdec_workload.hip"
+#include "tdec_spl.hip"
 
 using namespace tdec;
 
@@ -215,6 +216,7 @@ struct tdec_ctx {
     int cap_batch = 0;
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
     ConsCache cons;                    // demapper constellation
+    DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // copies of the chunked host-pointer path (created on first use)
     // Stream ordering of the handle-owned buffers (workspace, planes_own, cons,
@@ -377,6 +379,7 @@ void tdec_destroy(tdec_t *h) {
     h->h_lf.release();
     h->h_misc.release();
     h->cons.buf.release();
+    h->spl_ck.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->done_ev) hipEventDestroy(h->done_ev);
@@ -660,6 +663,8 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     double *deA = (double *)(base + 4 * cf + 2 * cd), *deB = (double *)(base + 4 * cf + 3 * cd);
     hipStream_t s = h->stream;
     const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
+    const char *se = getenv("TDEC_SISO_SPL");
+    const bool spl = se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
     for (long r0 = 0; r0 < B; r0 += C) {
         const int n = (int)std::min<long>(C, B - r0), nwv = n_tiles_of(n);
         const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(float), nd = (size_t)n * N * sizeof(double);
@@ -671,7 +676,13 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
         HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
         SisoArgs a{n, h->N, nwv, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
         const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-        if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
+        if (spl) {   // A/B prototype: one state per lane, 4 codewords per wave (tdec_spl.hip)
+            const long sw = (n + 3) / 4;                     // waves
+            const long stride = ((h->N + SPL_W - 1) / SPL_W + RING) * 64L;
+            if (int rc = h->spl_ck.ensure(sizeof(float) * stride * ((sw + 3) / 4 * 4))) return rc;
+            SplArgs sa{n, h->N, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float *)h->spl_ck.p, stride};
+            hipLaunchKernelGGL(k_siso_spl, dim3((unsigned)((sw + 3) / 4)), dim3(256), 0, s, sa);
+        } else if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
         else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
         else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
         else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);

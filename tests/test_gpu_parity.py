@@ -463,3 +463,19 @@ def test_host_decode_in_chunks(monkeypatch):
     for b in (0, 69, 70, 139, 140, 150):
         rA, rB = O.siso(*Lc[:, b], *La[:, b], t, 0.7)
         assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b
+
+
+@pytest.mark.parametrize("n", [48, 212, 752, 37])
+def test_state_per_lane_siso_prototype_bit_exact(monkeypatch, n):
+    """The north star's mapping (one state per lane, tdec_spl.hip), kept as a
+    timed A/B prototype: same SISO bits as the oracle."""
+    monkeypatch.setenv("TDEC_SISO_SPL", "1")
+    rng = np.random.default_rng(n)
+    t, _ = O.trellis()
+    B = 37
+    Lc = (rng.standard_normal((4, B, n)) * 3).astype(np.float32)
+    La = rng.standard_normal((2, B, n)) * 6
+    LeA, LeB = M.bcjr_max_log_map_batch(*Lc, *La, *_tabs(), n, 0.7)
+    for b in (0, 17, B - 1):
+        rA, rB = O.siso(Lc[0, b], Lc[1, b], Lc[2, b], Lc[3, b], La[0, b], La[1, b], t, 0.7)
+        assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b

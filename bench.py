@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--algo", default="max-log")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--fused", action="store_true", help="one launch (k_turbo_decode_syms, demap inside the "
+                    "decoder waves) instead of k_demap_planes + k_turbo_decode (A/B; measured slower)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
                     "several ranks on one GPU together with --all-on-device0")
     ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
@@ -191,7 +193,7 @@ def main():
     cw0 = rank * B                                   # this rank's global codewords: [rank*B, (rank+1)*B)
     t0 = time.time()
     # decoder workspace and planes first, into unfragmented HBM (placement)
-    pipe = DevicePipeline(codec, args.mod, B, device)
+    pipe = DevicePipeline(codec, args.mod, B, device, fused=args.fused)
     _, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, SEED, device, cw0=cw0, want_info=False)
     S = syms.shape[1]
     nv = np.float64(n0)

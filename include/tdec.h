@@ -125,6 +125,19 @@ int tdec_constellation(int mod, double *iq, int *is_f64);
 int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
                           int bps, double noise_var, int div_f32, float *d_planes, void *stream);
 
+/* Fused soft demap + turbo decode (one launch): what tdec_demap_planes_dev +
+ * tdec_decode_planes_dev compute, bit for bit, with each persistent decoder wave
+ * demapping its own next tile into a per-wave plane buffer.  Instantiated for
+ * the BASELINE configurations: max-log with complex64 tables of 4 or 8 bits per
+ * symbol (16QAM, 256QAM) or complex128 with 2 (QPSK), log-MAP with complex64
+ * and 3 (8PSK); tdec_fused_available() says whether a (table dtype, bps) pair
+ * has one (TDEC_EUNSUPPORTED otherwise).  tdec_reserve_fused sizes the
+ * workspace and the per-wave planes for batches of up to max_batch. */
+int tdec_reserve_fused(tdec_t *h, int max_batch);
+int tdec_fused_available(const tdec_t *h, int cons_f64, int bps);
+int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
+                          int bps, double noise_var, int div_f32, int32_t *d_bits, double *d_lfinal, void *stream);
+
 /* Batched encoder (workload generation): encode (dvb_rcs2_turbo.py:404-462)
  * with the handle's perm, bits uint8[B][2N] -> coded uint8[B][n_out],
  * n_out = the reference encoder's output length. */

@@ -217,6 +217,7 @@ struct tdec_ctx {
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
+    DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // copies of the chunked host-pointer path (created on first use)
     // Stream ordering of the handle-owned buffers (workspace, planes_own, cons,
@@ -380,6 +381,7 @@ void tdec_destroy(tdec_t *h) {
     h->h_misc.release();
     h->cons.buf.release();
     h->spl_ck.release();
+    h->planes_w.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->done_ev) hipEventDestroy(h->done_ev);
@@ -862,6 +864,64 @@ int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const in
                        seed, d_bits, d_errs);
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+// ---- fused demap + decode (k_turbo_decode_syms) ---------------------------------------
+typedef void (*fused_fn)(DecodeArgs, const int *, const int *, FusedDemapArgs);
+
+// The instantiated (algorithm, symbol dtype, bits per symbol) combinations: the
+// BASELINE configurations (QPSK / 16QAM / 256QAM max-log, 8PSK log-MAP); anything
+// else runs k_demap_planes + k_turbo_decode.
+static const void *fused_kernel(int algo, bool ragged, bool f64, int bps) {
+    if (ragged) return nullptr;
+    if (algo == 0 && !f64 && bps == 4) return (const void *)k_turbo_decode_syms<0, false, float, 4>;
+    if (algo == 0 && !f64 && bps == 8) return (const void *)k_turbo_decode_syms<0, false, float, 8>;
+    if (algo == 0 && f64 && bps == 2) return (const void *)k_turbo_decode_syms<0, false, double, 2>;
+    if (algo == 1 && !f64 && bps == 3) return (const void *)k_turbo_decode_syms<1, false, float, 3>;
+    return nullptr;
+}
+
+static int waves_for(const tdec_t *h, int B) { return std::min(n_tiles_of(B), h->max_waves); }
+
+int tdec_reserve_fused(tdec_t *h, int max_batch) {
+    if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
+    if (max_batch == 0) return 0;
+    Guard g(h->device);
+    const int w = waves_for(h, max_batch);
+    const size_t pw = 2 * (size_t)w * tile_floats(h->N) * sizeof(float);
+    if (w > h->ws_waves || pw > h->planes_w.cap) quiesce(h);
+    int rc = ensure_ws(h, w);
+    if (!rc) rc = h->planes_w.ensure(pw);
+    return rc;
+}
+
+int tdec_fused_available(const tdec_t *h, int cons_f64, int bps) {
+    return h && fused_kernel(h->algo, h->N % win_of(h->algo) != 0, cons_f64 != 0, bps) != nullptr;
+}
+
+int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
+                          int bps, double noise_var, int div_f32, int32_t *d_bits, double *d_lfinal, void *stream) {
+    if (!h || B < 0 || !cons) return fail(TDEC_EINVAL, "bad demap-decode arguments");
+    if (int rc = check_demap_args(M, bps)) return rc;
+    if (B == 0) return 0;
+    if (!d_syms || !d_bits || S <= 0) return fail(TDEC_EINVAL, "bad demap-decode arguments");
+    const void *k = fused_kernel(h->algo, h->N % win_of(h->algo) != 0, cons_f64 != 0, bps);
+    if (!k) return fail(TDEC_EUNSUPPORTED, "no fused demap-decode kernel for this modulation / algorithm");
+    Guard g(h->device);
+    const int tiles = n_tiles_of(B), waves = waves_for(h, B);
+    if (waves > h->ws_waves || 2 * (size_t)waves * tile_floats(h->N) * sizeof(float) > h->planes_w.cap)
+        return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve_fused first");
+    hipStream_t st = (hipStream_t)stream;
+    if (int rc = order_on(h, st)) return rc;
+    if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal};
+    FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
+                      (const int *)h->d_off, (float *)h->planes_w.p,
+                      DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};
+    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    hipLaunchKernelGGL((fused_fn)k, grid, dim3(BLOCK), 0, st, a, (const int *)h->d_perm, (const int *)h->d_inv, fa);
+    HIPCHK(hipGetLastError());
+    return mark_used(h, st);
 }
 
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream) {

@@ -997,10 +997,23 @@ struct DecodeArgs {
 #ifndef TDEC_EPI_LDS
 #define TDEC_EPI_LDS 1
 #endif
-template <int ALGO, bool RAG>
+// Where a tile's planes come from.  PlanesIn: the caller's plane buffer
+// (tdec_decode_planes_dev); fill / publish are no-ops.  The fused demap
+// (DemapPro, below) fills a wave's next tile piece by piece between the SISOs of
+// the current one, into the other of its two plane buffers.
+struct PlanesIn {
+    const float *planes;
+    __device__ __forceinline__ const float *tile_planes(int tile, int /*wave*/, int N, int /*buf*/) const {
+        return planes + (long)tile * tile_floats(N);
+    }
+    __device__ __forceinline__ void fill(int, int, int, int, int, int) const {}
+    __device__ __forceinline__ void publish() const {}
+};
+
+template <int ALGO, bool RAG, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, float4 *lv, double2 *ll,
-                                                   uint32_t *epi) {
+                                                   uint32_t *epi, const Pro &pro = Pro{}) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
@@ -1012,17 +1025,24 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     const int nw = (N + WIN_MIN - 1) / WIN_MIN;
     float4 *ck = p.ck + (long)wave * WAVE;
     float4 *ring = ck + (long)nw * 4 * rs;
+    int buf = 0;
+    pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
+    pro.publish();
     for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
-        const float *base = p.planes + (long)tile * tile_floats(N);
+        const float *base = pro.tile_planes(tile, wave, N, buf);
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
+        const int nxt = tile + p.n_waves;
+        const bool has_next = nxt < p.n_tiles;
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
             run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs}, N, ck, ring, rs, lane, sf, lv, ll);
+            if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf,
                                 lv, ll);
+            if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
@@ -1087,6 +1107,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             }
         }
 #endif
+        if (has_next) pro.publish();
+        buf ^= 1;
     }
 }
 
@@ -1103,7 +1125,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_W
     __shared__ float4 lv[LDS_STAGE];
     __shared__ double2 ll[LDS_STAGE];
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
-    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll, epi);
+    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll, epi, PlanesIn{p.planes});
 }
 #ifndef TDEC_LM_WPE
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
@@ -1112,7 +1134,7 @@ template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
-    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr, epi);
+    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr, epi, PlanesIn{p.planes});
 }
 
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).
@@ -1398,6 +1420,101 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
         else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
     }
+}
+
+// ---- fused demap + decode ------------------------------------------------------------
+// Each persistent decoder wave demaps its next 64-codeword tile itself (the same
+// operations as k_demap_planes, so the planes are bit-identical) into a plane
+// buffer of its own, then decodes it.  The demap is VALU-bound and the decoder
+// HBM-bound, so inside one launch the demap's arithmetic runs while the other
+// waves stream the decoder's planes (a separate k_demap_planes launch serialises
+// them), and the plane buffer is sized per resident wave, not per codeword.
+constexpr int DF_KC = 8;                   // couples per LDS chunk
+constexpr int DF_LD = DF_KC * 6 + 1;       // odd row stride
+
+struct FusedDemapArgs {
+    const float *syms;                     // [B][S] complex64
+    int S;
+    long n_avail;                          // LLRs the symbols provide (<= the de-puncture walk)
+    const int *src, *off;                  // de-puncture map (tdec_create)
+    float *planes_w;                       // [n_waves][2] x tile_floats(N): the wave's current and next tile
+    DemapCfg c;
+    const void *cons_g;                    // device table (T)
+};
+
+template <typename T, int BPS> struct DemapPro {
+    FusedDemapArgs a;                       // by value: SGPRs, no address of a kernel argument
+    int B;
+    const T *cons;                          // LDS copy
+    float *L;                               // this wave's LDS chunk [64][DF_LD]
+    __device__ __forceinline__ const float *tile_planes(int /*tile*/, int wave, int N, int buf) const {
+        return a.planes_w + (2L * wave + buf) * tile_floats(N);
+    }
+    // chunks [piece/npieces, (piece+1)/npieces) of the tile's DF_KC-couple chunks
+    __device__ __forceinline__ void fill(int tile, int wave, int N, int buf, int piece, int npieces) const {
+        const int lane = threadIdx.x & (WAVE - 1);
+        float *pl = a.planes_w + (2L * wave + buf) * tile_floats(N);
+        float4 *X = reinterpret_cast<float4 *>(pl);
+        float2 *Z = reinterpret_cast<float2 *>(pl + (long)N * WAVE * 4);
+        const int S = a.S;
+        const int nch = (N + DF_KC - 1) / DF_KC;
+        const int c0 = piece * nch / npieces, c1 = (piece + 1) * nch / npieces;
+        for (int ch = c0; ch < c1; ++ch) {
+            const int k0 = ch * DF_KC, k1 = min(N, k0 + DF_KC);
+            const long j0 = a.off[k0], j1 = a.off[k1];
+            const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;   // symbols covering [j0, j1)
+            const int ns = (int)(s1 - s0);
+            for (int t = lane; t < WAVE * ns; t += WAVE) {
+                const int l = t / ns, si = t - l * ns;              // consecutive lanes: consecutive symbols
+                const long cw = (long)tile * WAVE + l;
+                const long sy = s0 + si;
+                if (cw >= B || sy >= S) continue;
+                const float2 z = *reinterpret_cast<const float2 *>(a.syms + 2 * (cw * S + sy));
+                double v[BPS];
+                demap_sym<T, BPS>((T)z.x, (T)z.y, cons, a.c, v);
+#pragma unroll
+                for (int b = 0; b < BPS; ++b) {
+                    const long j = sy * BPS + b;
+                    if (j >= j0 && j < j1) L[l * DF_LD + (int)(j - j0)] = (float)v[b];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const long cw = (long)tile * WAVE + lane;
+            for (int k = k0; k < k1; ++k) {
+                float v[6];
+#pragma unroll
+                for (int cc = 0; cc < 6; ++cc) {
+                    const int j = a.src[(long)(cc < 4 ? cc : cc + 2) * N + k];
+                    v[cc] = (j >= 0 && j < a.n_avail && cw < B) ? L[lane * DF_LD + (int)(j - j0)] : 0.0f;
+                }
+                X[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+                Z[(long)k * WAVE + lane] = make_float2(v[4], v[5]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    // the decoder reads the filled planes back through the CU's vector L1, which
+    // may hold lines of the buffer's previous tile: publish the stores, invalidate L1
+    __device__ __forceinline__ void publish() const {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+};
+
+template <int ALGO, bool RAG, typename T, int BPS>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ALGO ? TDEC_LM_WPE : TDEC_ML_WPE))) void
+k_turbo_decode_syms(DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, FusedDemapArgs fa) {
+    __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+    __shared__ T cons[DM_TAB];
+    __shared__ float L[WAVES_PER_BLOCK * WAVE * DF_LD];
+    load_table<T, BPS>(cons, reinterpret_cast<const T *>(fa.cons_g), fa.c);
+    __syncthreads();
+    DemapPro<T, BPS> pro{fa, p.B, cons, L + (threadIdx.x >> 6) * WAVE * DF_LD};
+    turbo_decode_tiles<ALGO, RAG>(p, perm, inv, nullptr, nullptr, epi, pro);
 }
 
 // ---- encoder (workload generation; encode, :404-462) ------------------------------

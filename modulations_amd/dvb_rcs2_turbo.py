@@ -292,6 +292,31 @@ class DVBRCS2_Turbo:
                          float(noise_var), int(div_f32), _n.ptr(planes), self._stream(stream))
         return planes
 
+    # -- fused demap + decode (one launch; tdec_demap_decode_dev) -------------------------
+    def fused_available(self, constellation, bps):
+        cons = np.asarray(constellation)
+        return bool(_n.lib().tdec_fused_available(self.handle.h, int(cons.dtype == np.complex128), int(bps)))
+
+    def reserve_fused(self, max_batch):
+        self.handle.call("tdec_reserve_fused", int(max_batch))
+
+    def demap_decode_device(self, syms, constellation, bps, noise_var, bits, lfinal=None, div_f32=False,
+                            stream=None):
+        """compute_llr (decoder sign) -> f32 -> decode of complex64 symbols [B, S] in one
+        launch: the bits of demap_planes_device + decode_planes_device."""
+        import torch
+        cons = np.ascontiguousarray(np.asarray(constellation))
+        f64 = cons.dtype == np.complex128
+        cons = cons.astype(np.complex128 if f64 else np.complex64)
+        self._dev_check(syms, "syms", torch.complex64)
+        B, S = syms.shape[0], syms.shape[1]
+        self._dev_check(bits, "bits", torch.int32, (B, self.k_info))
+        if lfinal is not None:
+            self._dev_check(lfinal, "lfinal", torch.float64, (B, self.k_info))
+        self.handle.call("tdec_demap_decode_dev", B, _n.ptr(syms), S, _n.ptr(cons), int(f64), len(cons), bps,
+                         float(noise_var), int(div_f32), _n.ptr(bits), _n.ptr(lfinal), self._stream(stream))
+        return bits
+
     def encode_device(self, bits_u8, coded_u8=None, stream=None):
         """Batched device encoder: uint8 [B, 2N] -> uint8 [B, n_out] (same bits as encode())."""
         import torch

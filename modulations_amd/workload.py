@@ -70,27 +70,44 @@ def _ptr(t):
 
 
 class DevicePipeline:
-    """Fused demap -> turbo decode over device-resident symbols (the bench step).
+    """Demap -> turbo decode over device-resident symbols (the bench step).
 
-    Buffers are sized once (tdec_reserve + planes + bits); run() is
-    stream-ordered and allocation free."""
+    Default: the two launches k_demap_planes + k_turbo_decode over a plane
+    buffer.  fused=True uses the one-launch k_turbo_decode_syms (each decoder
+    wave demaps its next tile between the SISOs of the current one) where the
+    handle has it; the bits are the same either way.  The fused launch measured
+    3-4 % SLOWER on MI355X (294 vs 285 ms per 1 M codewords): a
+    wave that demaps is not streaming, and at two waves per SIMD the decoder
+    needs every wave streaming to keep HBM busy.  Buffers are sized once; run()
+    is stream-ordered and allocation free."""
 
-    def __init__(self, codec, mod, B, device):
+    def __init__(self, codec, mod, B, device, fused=False):
         import torch
         self.codec, self.mod, self.B = codec, mod, B
         self.bps = D.MODULATIONS[mod]["bps"]
         self.cons = D.constellation(mod)
-        codec.reserve(B)
-        self.planes = torch.empty(codec.planes_bytes(B) // 4, dtype=torch.float32, device=device)
+        self.fused = bool(fused) and codec.fused_available(self.cons, self.bps)
+        if self.fused:
+            codec.reserve_fused(B)
+            self.planes = None
+        else:
+            codec.reserve(B)
+            self.planes = torch.empty(codec.planes_bytes(B) // 4, dtype=torch.float32, device=device)
         self.bits = torch.empty((B, codec.k_info), dtype=torch.int32, device=device)
 
     def run(self, syms, noise_var, stream=None, events=None):
         _, div32, nve = D.demap_mode(np.complex64, self.cons.dtype, np.float64(noise_var))
-        self.codec.demap_planes_device(syms, self.cons, self.bps, nve, self.planes, div_f32=div32, stream=stream)
-        if events is not None:
-            events[0].record(stream)
         bits = self.bits[:syms.shape[0]]          # the first rows: a contiguous view
-        self.codec.decode_planes_device(self.planes, syms.shape[0], bits, stream=stream)
+        if self.fused:
+            if events is not None:
+                events[0].record(stream)
+            self.codec.demap_decode_device(syms, self.cons, self.bps, nve, bits, div_f32=div32, stream=stream)
+        else:
+            self.codec.demap_planes_device(syms, self.cons, self.bps, nve, self.planes, div_f32=div32,
+                                           stream=stream)
+            if events is not None:
+                events[0].record(stream)
+            self.codec.decode_planes_device(self.planes, syms.shape[0], bits, stream=stream)
         if events is not None:
             events[1].record(stream)
         return bits

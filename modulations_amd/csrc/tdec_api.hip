@@ -207,6 +207,7 @@ struct tdec_ctx {
     int circ[16] = {0};
     int max_waves = 0;                 // resident waves of the decode kernel on this device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
+    int32_t *d_used = nullptr;         // [N]: k in the image of perm
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
@@ -330,7 +331,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     for (int z = 0; z < 16; ++z) h->circ[z] = solve_circ(res, z);
 
     hipError_t e = hipSuccess;
+    std::vector<int32_t> used(N, 0);
+    for (int k = 0; k < N; ++k) used[perm[k]] = 1;
     e = hipMalloc(&h->d_perm, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMalloc(&h->d_used, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMemcpy(h->d_used, used.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
@@ -370,6 +375,7 @@ void tdec_destroy(tdec_t *h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->pending) hipEventSynchronize(h->done_ev);
     hipFree(h->d_perm);
+    hipFree(h->d_used);
     hipFree(h->d_inv);
     hipFree(h->d_src);
     hipFree(h->d_off);
@@ -408,7 +414,7 @@ static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) /
 static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, const float *planes, int32_t *bits,
                              hipEvent_t e0, hipEvent_t e1) {
     const int B = waves * WAVE;
-    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr};
+    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
     float best = 1e30f;
@@ -544,7 +550,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipStream_t st = (hipStream_t)stream;
@@ -914,7 +920,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};

@@ -478,12 +478,19 @@ struct TileInPre {
 
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
 // iteration) Le1 itself for the final decision (:529-530).
+// P1[k] is read by decoder 2 only as P1[perm[k']]: perm is not a permutation
+// (355 distinct values of 752 at N = 752), so rows outside its image are never
+// read and are not written (used[k] = 0): 53 % of the P1 stream at N = 752.
+#ifndef TDEC_P1_ALL
+#define TDEC_P1_ALL 0
+#endif
 struct TileOutPre {
     double2 *P, *Le;   // Le may be null
     int lane;
     unsigned rs;
+    const int *__restrict__ used;
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
-        at(P, k * rs + lane) = make_double2((double)lcA + a, (double)lcB + b);
+        if (TDEC_P1_ALL || used[k]) at(P, k * rs + lane) = make_double2((double)lcA + a, (double)lcB + b);
         if (Le) at(Le, k * rs + lane) = make_double2(a, b);
     }
 };
@@ -991,6 +998,7 @@ struct DecodeArgs {
     float4 *ck;              // [ceil(N/WIN) + RING][4][n_waves][64]: alpha checkpoints, beta1 ring
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
+    const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1038,7 +1046,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
             run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
-                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs}, N, ck, ring, rs, lane, sf, lv, ll);
+                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs, p.p1_used}, N, ck, ring, rs, lane, sf,
+                                lv, ll);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf,
                                 lv, ll);

@@ -479,3 +479,18 @@ def test_state_per_lane_siso_prototype_bit_exact(monkeypatch, n):
     for b in (0, 17, B - 1):
         rA, rB = O.siso(Lc[0, b], Lc[1, b], Lc[2, b], Lc[3, b], La[0, b], La[1, b], t, 0.7)
         assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b
+
+
+def test_reference_test_py_recipe_through_the_drop_in():
+    """The reference's test.py recipe (QPSK r=1/2 N=752 8 iterations, its
+    -(2 sqrt 2)/N0 LLR scale) through DVBRCS2_Turbo exactly as test.py calls it
+    (codec.decode(llrs) per frame) and as a batch: the reference's bits."""
+    from conftest import golden
+    g = golden("testpy")
+    c = M.DVBRCS2_Turbo(752, "1/2", 8, inv_perm="numpy-avx512")
+    assert np.array_equal(c.inv_perm, g["inv_perm"])
+    llrs = np.stack([g[f"llr_{i}"] for i in range(9)])
+    want = np.stack([g[f"bits_{i}"] for i in range(9)])
+    assert np.array_equal(c.decode_batch(llrs), want)
+    for i in (0, 8):
+        assert np.array_equal(c.decode(g[f"llr_{i}"]), g[f"bits_{i}"])

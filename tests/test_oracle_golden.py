@@ -7,6 +7,7 @@ The golden vectors were produced by importing the reference module itself
 import numpy as np
 import pytest
 
+from conftest import golden
 from oracle import oracle as O
 from modulations_amd import tables as T
 
@@ -180,3 +181,16 @@ def test_logmap_siso_within_1e5_of_exact_log_map():
         big = max(np.max(np.abs(Lc[0] + La[0])), np.max(np.abs(Lc[1] + La[1])))
         for x, r in ((A, RA), (B, RB)):
             assert np.max(np.abs(x - r)) <= 1e-5 + 2 * 2.0 ** -23 * big, trial
+
+
+def test_oracle_replays_reference_test_py_recipe():
+    """test.py (Waveform 14: QPSK r=1/2 N=752, LLR scale -(2 sqrt 2)/N0, the
+    script's own sign) replayed through the reference: the oracle decodes the
+    recorded LLRs to the reference's bits (tests/golden/make_golden_testpy.py)."""
+    g = golden("testpy")
+    t, _ = O.trellis()
+    perm = T.interleaver(752)
+    pm = T.puncture_matrix(T.PUNCTURE_PATTERNS["1/2"])
+    for i in range(9):
+        rb = O.decode_batch(g[f"llr_{i}"][None], 752, 2, pm, 8, perm, g["inv_perm"], t)
+        assert np.array_equal(rb[0], g[f"bits_{i}"]), i

@@ -213,6 +213,7 @@ struct tdec_ctx {
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
+    int row_pad = 0;   // TDEC_ROW_PAD (placement study): lanes of padding per workspace row
     DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
     int cap_batch = 0;
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
@@ -355,6 +356,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
         return fail(TDEC_EHIP, std::string("tdec_create: ") + hipGetErrorString(e));
     }
     h->max_waves = std::max(1, blocks_per_cu) * n_cu * WAVES_PER_BLOCK;
+    if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
     const long row_units = std::max<long>(N, 4L * ((N + WIN_MIN - 1) / WIN_MIN + RING));
@@ -414,7 +416,8 @@ static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) /
 static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, const float *planes, int32_t *bits,
                              hipEvent_t e0, hipEvent_t e1) {
     const int B = waves * WAVE;
-    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used};
+    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used,
+                 h->row_pad};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
     float best = 1e30f;
@@ -453,13 +456,27 @@ constexpr float FAST_VS_MEDIAN = 0.97f;
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
     const size_t MB2 = 2u << 20;
-    const size_t le_bytes = (size_t)waves * ws_stride_of(h) * sizeof(double2);
+    // rows of waves*64 lanes (+ row_pad): the planes have 3N rows, the checkpoints ck_stride_of / 64
+    const size_t row = (size_t)waves * WAVE + h->row_pad;
+    const size_t le_bytes = row * (ws_stride_of(h) / WAVE) * sizeof(double2);
     const size_t ck_off = (le_bytes + MB2 - 1) / MB2 * MB2;
-    const size_t total = ck_off + (size_t)waves * ck_stride_of(h) * sizeof(float4);
+    const size_t total = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
     const char *pe = getenv("TDEC_PLACEMENT_PROBE");
     const bool probe = !(pe && pe[0] == '0') && waves == h->max_waves && total >= (1ul << 30);
     if (!probe) {
-        if (int rc = h->ws.ensure(total)) return rc;
+        // measurement knob (placement study): TDEC_WS_ALLOC=contiguous allocates the
+        // workspace as one physically contiguous range
+        const char *wa = getenv("TDEC_WS_ALLOC");
+        if (wa && !strcmp(wa, "contiguous")) {
+            h->ws.release();
+            if (hipExtMallocWithFlags(&h->ws.p, total, hipDeviceMallocContiguous) != hipSuccess) {
+                h->ws.p = nullptr;
+                return fail(TDEC_ENOMEM, "hipExtMallocWithFlags(contiguous) failed (decoder workspace)");
+            }
+            h->ws.cap = total;
+        } else if (int rc = h->ws.ensure(total)) {
+            return rc;
+        }
     } else {
         h->ws.release();
         const char *pc = getenv("TDEC_PROBE_CANDIDATES");
@@ -550,7 +567,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipStream_t st = (hipStream_t)stream;
@@ -920,7 +937,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};

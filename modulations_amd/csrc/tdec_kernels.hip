@@ -999,6 +999,7 @@ struct DecodeArgs {
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
+    int row_pad;             // lanes of padding after each workspace row (0 unless TDEC_ROW_PAD)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1028,7 +1029,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     const int N = p.N;
     const long NW = (long)N * WAVE;
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
-    const unsigned rs = (unsigned)p.n_waves * WAVE;
+    const unsigned rs = (unsigned)p.n_waves * WAVE + (unsigned)p.row_pad;
     double2 *P1 = p.ws + (long)wave * WAVE, *Le2 = P1 + (long)N * rs, *Le1 = Le2 + (long)N * rs;
     const int nw = (N + WIN_MIN - 1) / WIN_MIN;
     float4 *ck = p.ck + (long)wave * WAVE;

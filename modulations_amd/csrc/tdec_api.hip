@@ -191,7 +191,7 @@ int check_demap_args(int M, int bps) {
     return 0;
 }
 
-typedef void (*decode_fn)(DecodeArgs, const int *, const int *);
+typedef void (*decode_fn)(DecodeArgs, const int *, const int *, const int *);
 
 const void *decode_kernel(int algo, bool ragged) {
     if (algo) return ragged ? (const void *)k_turbo_decode_logmap<true> : (const void *)k_turbo_decode_logmap<false>;
@@ -211,6 +211,7 @@ struct tdec_ctx {
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
+    double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
     int row_pad = 0;   // TDEC_ROW_PAD (placement study): lanes of padding per workspace row
@@ -359,7 +360,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
-    const long row_units = std::max<long>(N, 4L * ((N + WIN_MIN - 1) / WIN_MIN + RING));
+    const long row_units = std::max<long>(rows_of(N), 4L * ((N + WIN_MIN - 1) / WIN_MIN + RING));
     const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
     h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
     // experiment knob: run the persistent decoder on a percentage of the resident waves
@@ -408,23 +409,24 @@ size_t tdec_planes_bytes(const tdec_t *h, int B) {
 static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 
 // Per-wave workspace strides (elements).
-static long ws_stride_of(const tdec_t *h) { return 3L * h->N * WAVE; }
+static long ws_stride_of(const tdec_t *h) { return 3L * rows_of(h->N) * WAVE; }
 static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) / WIN_MIN + RING) * 4 * WAVE; }
 
 // Time one single-iteration decode of waves*64 codewords of constant LLRs on a
 // candidate workspace (the placement probe below).
-static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, const float *planes, int32_t *bits,
+static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size_t aux_off, const float *planes,
+                             int32_t *bits,
                              hipEvent_t e0, hipEvent_t e1) {
     const int B = waves * WAVE;
     DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used,
-                 h->row_pad};
+                 h->row_pad, (double2 *)(ws + aux_off)};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
     float best = 1e30f;
     for (int rep = 0; rep < 2; ++rep) {
         hipEventRecord(e0, h->stream);
         hipLaunchKernelGGL((decode_fn)k, grid, dim3(BLOCK), 0, h->stream, a, (const int *)h->d_perm,
-                           (const int *)h->d_inv);
+                           (const int *)h->d_inv, (const int *)h->d_used);
         hipEventRecord(e1, h->stream);
         if (hipEventSynchronize(e1) != hipSuccess) return 1e30f;
         float ms = 0.0f;
@@ -460,7 +462,10 @@ static int ensure_ws(tdec_t *h, int waves) {
     const size_t row = (size_t)waves * WAVE + h->row_pad;
     const size_t le_bytes = row * (ws_stride_of(h) / WAVE) * sizeof(double2);
     const size_t ck_off = (le_bytes + MB2 - 1) / MB2 * MB2;
-    const size_t total = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
+    // aux: the all-zero a-priori row of the first iteration (64 lanes, zeroed
+    // below) and one sink row per wave for the stores the decoder discards
+    const size_t aux_off = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
+    const size_t total = aux_off + ((size_t)WAVE + row) * sizeof(double2);
     const char *pe = getenv("TDEC_PLACEMENT_PROBE");
     const bool probe = !(pe && pe[0] == '0') && waves == h->max_waves && total >= (1ul << 30);
     if (!probe) {
@@ -493,8 +498,10 @@ static int ensure_ws(tdec_t *h, int waves) {
         bool timed = false;
         for (int round = 0; round < 2; ++round) {
             const int first = n, want = std::min(cap, first + (round ? per_round : std::min(per_round, cap / 2 + 1)));
-            for (; n < want; ++n)
+            for (; n < want; ++n) {
                 if (hipMalloc(&cand[n], total) != hipSuccess) break;
+                hipMemsetAsync((char *)cand[n] + aux_off, 0, WAVE * sizeof(double2), h->stream);
+            }
             if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
             if (n == 1) break;
             if (!timed) {
@@ -505,7 +512,8 @@ static int ensure_ws(tdec_t *h, int waves) {
                 if (!timed) break;
             }
             for (int i = first; i < n; ++i) {
-                ms[i] = probe_decode_ms(h, waves, (char *)cand[i], ck_off, (const float *)planes, (int32_t *)bits, e0,
+                ms[i] = probe_decode_ms(h, waves, (char *)cand[i], ck_off, aux_off, (const float *)planes,
+                                        (int32_t *)bits, e0,
                                         e1);
                 if (ms[i] < ms[best]) best = i;
             }
@@ -529,6 +537,9 @@ static int ensure_ws(tdec_t *h, int waves) {
     }
     h->le_p = (double2 *)h->ws.p;
     h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
+    h->aux_p = (double2 *)((char *)h->ws.p + aux_off);
+    HIPCHK(hipMemsetAsync(h->aux_p, 0, WAVE * sizeof(double2), h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
     h->ws_waves = waves;
     return 0;
 }
@@ -567,13 +578,14 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
+                 h->aux_p};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, st,
-                       a, pm, iv);
+                       a, pm, iv, (const int *)h->d_used);
     HIPCHK(hipGetLastError());
     return mark_used(h, st);
 }
@@ -890,7 +902,7 @@ int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const in
 }
 
 // ---- fused demap + decode (k_turbo_decode_syms) ---------------------------------------
-typedef void (*fused_fn)(DecodeArgs, const int *, const int *, FusedDemapArgs);
+typedef void (*fused_fn)(DecodeArgs, const int *, const int *, const int *, FusedDemapArgs);
 
 // The instantiated (algorithm, symbol dtype, bits per symbol) combinations: the
 // BASELINE configurations (QPSK / 16QAM / 256QAM max-log, 8PSK log-MAP); anything
@@ -937,12 +949,14 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad};
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
+                 h->aux_p};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL((fused_fn)k, grid, dim3(BLOCK), 0, st, a, (const int *)h->d_perm, (const int *)h->d_inv, fa);
+    hipLaunchKernelGGL((fused_fn)k, grid, dim3(BLOCK), 0, st, a, (const int *)h->d_perm, (const int *)h->d_inv,
+                       (const int *)h->d_used, fa);
     HIPCHK(hipGetLastError());
     return mark_used(h, st);
 }

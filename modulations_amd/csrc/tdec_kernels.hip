@@ -375,6 +375,12 @@ template <class T> __device__ __forceinline__ const T &at(const T *base, unsigne
 }
 
 // ---- per-lane SISO --------------------------------------------------------------
+// Workspace rows (P1, Le2, Le1 planes; alpha checkpoints): [k][wave][64].  A
+// layout with the rows of 4 consecutive steps contiguous per wave
+// ([k/4][wave][k%4][64]) was measured 1 % slower (round 2).
+constexpr int WS_G = 1;
+__device__ __forceinline__ unsigned wsrow(unsigned k, unsigned rs) { return k * rs; }
+__host__ __device__ constexpr int rows_of(int N) { return N; }
 // Raw branch inputs of one trellis step, 32 B per lane as two 16-B loads:
 //   plain:      v = {Lc_A, Lc_B, Lc_W, Lc_Y} (f32), l = {La_A, La_B} (f64)
 //   pre-summed: v = {-, -, Lc_W, Lc_Y},          l = {inA, inB} = f64(Lc) + La
@@ -399,6 +405,9 @@ __device__ __forceinline__ void glds4(const void *g, void *l) {
 // (the 4 extrinsic stores of the bottom half and the 4 checkpoint loads of the
 // next window), so this retires the DMA without waiting for those stores.
 __device__ __forceinline__ void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70 | 8); }
+// s_waitcnt vmcnt(n) for the double-buffered staging: n = the LDS-DMA operations
+// of the NEXT window's stage (issued last), so everything older has retired.
+template <int n> __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70 | n); }
 
 // A wave's staged half window: 4 steps x {16-B plane v, 16-B plane l} x 64 lanes.
 struct LdsStage {
@@ -409,8 +418,10 @@ struct LdsStage {
 
 // Decoder 1 in the tile layout: X = [N][64] float4 {A, B, W1, Y1} (uniform
 // base), a-priori La = Le2[inv_perm[k]] ([N][64] double2, the same index for
-// every lane), or null for the all-zero a-priori of the first iteration
-// (:490-491).
+// every lane).  The all-zero a-priori of the first iteration (:490-491) is a
+// zero row read with row stride 0 (L2-resident), so the loads are the same
+// straight-line code in every iteration: no branch for the compiler's
+// wait-count analysis to merge pessimistically.
 struct TileIn {
     const float4 *X;
     const double2 *La;
@@ -420,7 +431,7 @@ struct TileIn {
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
         r.v = at(X, k * WAVE + lane);
-        r.l = La ? at(La, la_idx[k] * rs + lane) : make_double2(0.0, 0.0);
+        r.l = at(La, wsrow(la_idx[k], rs) + lane);
         return r;
     }
     __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
@@ -428,14 +439,16 @@ struct TileIn {
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
-        if (La) glds16(&at(La, la_idx[k] * rs + lane), st.l + j * WAVE);
+        glds16(&at(La, wsrow(la_idx[k], rs) + lane), st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         Raw r;
         r.v = st.v[j * WAVE + lane];
-        r.l = La ? st.l[j * WAVE + lane] : make_double2(0.0, 0.0);
+        r.l = st.l[j * WAVE + lane];
         return r;
     }
+    // retire all but the last stage's 4 x (X + La) DMA operations
+    __device__ __forceinline__ void wait_staged() const { wait_vm<8>(); }
 };
 
 // Decoder 2: the sums inA = f64(Lc_A[perm[k]]) + Le1_A[perm[k]] (:511-516)
@@ -451,7 +464,7 @@ struct TileInPre {
         Raw r;
         const float2 z = at(Z, k * WAVE + lane);
         r.v = make_float4(0.0f, 0.0f, z.x, z.y);
-        r.l = at(P, p_idx[k] * rs + lane);
+        r.l = at(P, wsrow(p_idx[k], rs) + lane);
         return r;
     }
     __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
@@ -465,7 +478,7 @@ struct TileInPre {
         float *dst = reinterpret_cast<float *>(st.v + j * WAVE);
         glds4(z, dst);
         glds4(z + 1, dst + WAVE);
-        glds16(&at(P, p_idx[k] * rs + lane), st.l + j * WAVE);
+        glds16(&at(P, wsrow(p_idx[k], rs) + lane), st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         const float *zp = reinterpret_cast<const float *>(st.v + j * WAVE);
@@ -474,6 +487,7 @@ struct TileInPre {
         r.l = st.l[j * WAVE + lane];
         return r;
     }
+    __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
 };
 
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
@@ -484,14 +498,22 @@ struct TileInPre {
 #ifndef TDEC_P1_ALL
 #define TDEC_P1_ALL 0
 #endif
+// A discarded store goes to the wave's sink row (L2-resident) instead of being
+// skipped: every position issues the same stores, so the count of memory
+// operations between a load and its use is the same on every path and the
+// compiler's s_waitcnt does not wait for stores it need not.
 struct TileOutPre {
     double2 *P, *Le;   // Le may be null
     int lane;
     unsigned rs;
     const int *__restrict__ used;
+    double2 *sink;     // this wave's sink row
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
-        if (TDEC_P1_ALL || used[k]) at(P, k * rs + lane) = make_double2((double)lcA + a, (double)lcB + b);
-        if (Le) at(Le, k * rs + lane) = make_double2(a, b);
+        // wave-uniform row selects (SGPR pairs), then the lane offset
+        double2 *rp = (TDEC_P1_ALL || used[k]) ? &at(P, wsrow(k, rs)) : sink;
+        double2 *rl = Le ? &at(Le, wsrow(k, rs)) : sink;
+        at(rp, (unsigned)lane) = make_double2((double)lcA + a, (double)lcB + b);
+        at(rl, (unsigned)lane) = make_double2(a, b);
     }
 };
 
@@ -500,7 +522,7 @@ struct TileOut {
     int lane;
     unsigned rs;
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
-        at(Le, k * rs + lane) = make_double2(a, b);
+        at(Le, wsrow(k, rs) + lane) = make_double2(a, b);
     }
 };
 
@@ -589,19 +611,19 @@ __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base,
 // forward pass is recomputed from the window checkpoint (the same f32
 // operations, so bit-exact): holding all W alpha vectors of a window costs
 // 16*W VGPRs, recomputing costs W(W-1)/2 extra steps of VALU, which this
-// HBM-bound kernel has to spare.  `raw` holds the window's inputs on entry and
-// the previous window's (prefetched) on exit.
-#ifndef TDEC_BPF
-#define TDEC_BPF 1
-#endif
+// HBM-bound kernel has to spare.
+// `raw` / `an` hold this window's inputs / alpha checkpoint on entry and the
+// next (lower) window's on exit.  Both are loaded at the START of the window,
+// before its extrinsic stores: vmcnt retires in issue order, so waiting for a
+// load issued after a store waits for the store too.  The loads are
+// unconditional (the last window re-loads its own rows), so the number of
+// memory operations issued after them is the same on every path and the
+// compiler's wait counts stay exact.
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, int len, Raw (&raw)[W],
-                                            float (&b)[NS], const float4 *ck, unsigned cs, int lane, double sf) {
+                                            float (&an)[NS], float (&b)[NS], const float4 *ck, unsigned cs, int lane,
+                                            int N, double sf) {
     // len = steps in this window (W except for a ragged top window when W does not divide N)
-    if (!TDEC_BPF) {
-#pragma unroll
-        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? k0 + min(j, len - 1) : k0 + j);
-    }
     float gw[W][8], lcA[W], lcB[W];
     double iAw[W], iBw[W];
 #pragma unroll
@@ -611,10 +633,13 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         lcB[j] = raw[j].v.y;
     }
     float a0[NS];
-    load_vec<true>(a0, ck, cs, (k0 / W) * 4, lane);
-    if (TDEC_BPF && k0 > 0) {
 #pragma unroll
-        for (int j = 0; j < W; ++j) raw[j] = in.load(k0 - W + j);
+    for (int s = 0; s < NS; ++s) a0[s] = an[s];
+    {
+        const int kn = k0 >= W ? k0 - W : 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(kn + j, N - 1) : kn + j);
+        load_vec<true>(an, ck, cs, (kn / W) * 4, lane);
     }
 #ifndef TDEC_MID
 #define TDEC_MID 1
@@ -669,6 +694,43 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 //       values are exact (a pass that has not merged by then runs to the end).
 // ck: alpha checkpoints [ceil(N/W)][4][64] float4; ring: beta1 [RING][4][64].
 // Any N >= 1: only the top window can be short, every guard is wave-uniform.
+// F1 of a SISO: alpha from a (zero) over all N steps, checkpoint every W steps,
+// inputs software-pipelined one group of FG steps ahead.  A deeper group than
+// W (FG = 8 at W = 4) measured no faster (round 2): F1's waits are already
+// covered, it is the backward windows that expose latency.
+#ifndef TDEC_FG
+#define TDEC_FG 4
+#endif
+template <int ALGO, int W, bool RAG, class In>
+__device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigned cs, int lane, float (&a)[NS]) {
+    constexpr int FG = TDEC_FG > W ? TDEC_FG : W;   // a multiple of W
+    static_assert(FG % W == 0, "FG must be a multiple of W");
+    // steps past N exist only when W does not divide N (RAG) or FG > W
+    const bool tail = RAG || (FG > W && N % FG != 0);
+    Raw raw[FG];
+#pragma unroll
+    for (int j = 0; j < FG; ++j) raw[j] = in.load(tail ? min(j, N - 1) : j);
+    for (int k0 = 0; k0 < N; k0 += FG) {
+        float g[FG][8];
+#pragma unroll
+        for (int j = 0; j < FG; ++j) {
+            if (tail && k0 + j >= N) continue;   // wave-uniform
+            double iA, iB;
+            in.gamma(raw[j], g[j], iA, iB);
+        }
+        if (k0 + FG < N) {
+#pragma unroll
+            for (int j = 0; j < FG; ++j) raw[j] = in.load(tail ? min(k0 + FG + j, N - 1) : k0 + FG + j);
+        }
+#pragma unroll
+        for (int j = 0; j < FG; ++j) {
+            if (tail && k0 + j >= N) continue;
+            if (j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
+            alpha_step<ALGO>(a, g[j]);
+        }
+    }
+}
+
 constexpr int RING = 16;   // beta1 kept at RING window starts 16 steps apart: the top 256 steps (merge: median 40, max 122)
 __host__ __device__ constexpr int rstep_of(int w) { return w >= 16 ? 1 : 16 / w; }
 
@@ -681,25 +743,8 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
-    // F1 (inputs software-pipelined one group of W steps ahead)
-#pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
-    for (int k0 = 0; k0 < N; k0 += W) {
-        float g[W][8];
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-            double iA, iB;
-            in.gamma(raw[j], g[j], iA, iB);
-        }
-        if (k0 + W < N) {
-#pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
-        }
-        store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
-#pragma unroll
-        for (int j = 0; j < W; ++j)
-            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
-    }
+    // F1 (inputs software-pipelined one group of FG steps ahead)
+    f1_pass<ALGO, W, RAG>(in, N, ck, cs, lane, a);
     // F2 until merged (a = alpha1[N] = alpha2[0]).  Per lane: once alpha2 ==
     // alpha1 at a checkpoint, every later checkpoint already holds alpha2, so
     // the lane stops loading and storing (masked lanes move no bytes); the
@@ -733,20 +778,22 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         }
     }
     // B1 fused with the provisional extrinsic
-    float b[NS];
+    float b[NS], an[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+    load_vec<true>(an, ck, cs, (top / W) * 4, lane);
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;                     // window index from the top
         if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
-        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
     }
     // B2 until merged (b = beta1[0] = beta2[N]); per lane as F2: below its
     // merge point a lane's provisional extrinsics are exact, it stops there
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+    load_vec<true>(an, ck, cs, (top / W) * 4, lane);
     merged = false;
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;
@@ -755,10 +802,10 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
                 if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP * 4, lane);
                 if (__all(merged)) break;
             }
-            if (!merged) back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+            if (!merged) back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
         } else {
             if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
-            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, b, ck, cs, lane, sf);
+            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
         }
     }
 }
@@ -809,14 +856,24 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 // half inputs on entry, the next (lower) window's on exit.  st: this window's
 // bottom half on entry (LDS-DMA issued during the previous window), the next
 // window's in flight on exit.
+// Double-buffered staging (TDEC_STAGE_DB): the next window's bottom half is
+// issued into the other buffer at the START of this window, a whole window
+// ahead of its use, instead of after this window's last LDS read.
+#ifndef TDEC_STAGE_DB
+#define TDEC_STAGE_DB 1
+#endif
 template <int ALGO, bool RAG, class In, class Out>
 __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k0, int len, Raw (&rt)[4],
-                                             const LdsStage &st, float (&b)[NS], const float4 *ck, unsigned cs,
-                                             int lane, double sf) {
+                                             const LdsStage &st, const LdsStage &sn, float (&b)[NS],
+                                             const float4 *ck, unsigned cs, int lane, double sf) {
     const int lenT = RAG ? (len > 4 ? len - 4 : 0) : 4;
     const int lenB = RAG ? (len < 4 ? len : 4) : 4;
     float a0[NS];
     load_vec<true>(a0, ck, cs, (k0 / 8) * 4, lane);
+    if (TDEC_STAGE_DB && k0 > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) in.stage(k0 - 8 + j, sn, j);
+    }
     if (!RAG || lenT > 0) {
         float gw[4][8], lcA[4], lcB[4];
         double iAw[4], iBw[4];
@@ -826,7 +883,9 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             lcA[j] = rt[j].v.x;
             lcB[j] = rt[j].v.y;
         }
-        wait_vm_all();   // the staged bottom half (and the checkpoint) have landed
+        // the staged bottom half (and the checkpoint) have landed
+        if (TDEC_STAGE_DB) in.wait_staged();
+        else wait_vm_all();
         float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
 #pragma unroll
         for (int s = 0; s < NS; ++s) a4[s] = a0[s];
@@ -843,7 +902,8 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
         }
         window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
     } else {
-        wait_vm_all();
+        if (TDEC_STAGE_DB) in.wait_staged();
+        else wait_vm_all();
         if (k0 > 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) rt[j] = in.load(k0 - 4 + j);
@@ -858,7 +918,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
         lcA[j] = r.v.x;
         lcB[j] = r.v.y;
     }
-    if (k0 > 0) {   // the next window's bottom half, straight into LDS (the reads above are consumed)
+    if (!TDEC_STAGE_DB && k0 > 0) {   // the next window's bottom half, straight into LDS (the reads above are consumed)
 #pragma unroll
         for (int j = 0; j < 4; ++j) in.stage(k0 - 8 + j, st, j);
     }
@@ -869,32 +929,15 @@ constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16
 
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
-                      const LdsStage &lb) {
+                      const LdsStage &lb, const LdsStage &lb1) {
     constexpr int G = 4, CK = 8;
     const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
     Raw raw[G];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
-    // F1: groups of 4 steps, inputs pipelined one group ahead, checkpoint every 8
-#pragma unroll
-    for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
-    for (int k0 = 0; k0 < N; k0 += G) {
-        float g[G][8];
-#pragma unroll
-        for (int j = 0; j < G; ++j) {
-            double iA, iB;
-            in.gamma(raw[j], g[j], iA, iB);
-        }
-        if (k0 + G < N) {
-#pragma unroll
-            for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(k0 + G + j, N - 1) : k0 + G + j);
-        }
-        if ((k0 & (CK - 1)) == 0) store_vec<true>(ck, cs, (k0 / CK) * 4, lane, a);
-#pragma unroll
-        for (int j = 0; j < G; ++j)
-            if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
-    }
+    // F1: inputs pipelined one group of FG steps ahead, checkpoint every 8
+    f1_pass<ALGO, CK, RAG>(in, N, ck, cs, lane, a);
     // F2 until merged with F1 at a checkpoint
 #pragma unroll
     for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
@@ -942,7 +985,11 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
                 if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane);
                 if (__all(merged)) break;
             }
-            if (!merged) back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, lb, b, ck, cs, lane, sf);
+            if (!merged) {
+                const bool odd = TDEC_STAGE_DB && (r & 1);
+                back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, odd ? lb1 : lb,
+                                        TDEC_STAGE_DB ? (odd ? lb : lb1) : lb, b, ck, cs, lane, sf);
+            }
         }
     }
 }
@@ -971,7 +1018,8 @@ constexpr int WIN_LM = TDEC_WIN_LM;      // log-MAP turbo decoder's checkpoint i
 __host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_ML; }
 // the workspace's checkpoint array is sized for the densest interval in use
 constexpr int WIN_MIN = WIN < WIN_ML ? (WIN < WIN_LM ? WIN : WIN_LM) : (WIN_ML < WIN_LM ? WIN_ML : WIN_LM);
-constexpr int LDS_STAGE = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of a block's staging planes
+constexpr int LDS_STAGE1 = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
+constexpr int LDS_STAGE = LDS_STAGE1 * (TDEC_STAGE_DB ? 2 : 1);
 
 // The SISO of the tile decoder: siso8 for max-log at WIN_ML 8, else siso<> at WIN.
 template <int ALGO, bool RAG, class In, class Out>
@@ -979,7 +1027,9 @@ __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, fl
                                          int lane, double sf, float4 *lv, double2 *ll) {
     if constexpr (ALGO == 0 && WIN_ML == 8) {
         const int w = threadIdx.x >> 6;
-        siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{lv + w * 4 * WAVE, ll + w * 4 * WAVE, lane});
+        siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{lv + w * 4 * WAVE, ll + w * 4 * WAVE, lane},
+                         LdsStage{lv + (TDEC_STAGE_DB ? LDS_STAGE1 : 0) + w * 4 * WAVE,
+                                  ll + (TDEC_STAGE_DB ? LDS_STAGE1 : 0) + w * 4 * WAVE, lane});
     } else {
         siso<ALGO, (ALGO ? WIN_LM : WIN_ML), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
@@ -1000,6 +1050,7 @@ struct DecodeArgs {
     double *lfinal;          // [B][2N] or null
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
     int row_pad;             // lanes of padding after each workspace row (0 unless TDEC_ROW_PAD)
+    double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1021,7 +1072,8 @@ struct PlanesIn {
 
 template <int ALGO, bool RAG, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
-                                                   const int *__restrict__ inv, float4 *lv, double2 *ll,
+                                                   const int *__restrict__ inv, const int *__restrict__ used,
+                                                   float4 *lv, double2 *ll,
                                                    uint32_t *epi, const Pro &pro = Pro{}) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
@@ -1030,10 +1082,11 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     const long NW = (long)N * WAVE;
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
     const unsigned rs = (unsigned)p.n_waves * WAVE + (unsigned)p.row_pad;
-    double2 *P1 = p.ws + (long)wave * WAVE, *Le2 = P1 + (long)N * rs, *Le1 = Le2 + (long)N * rs;
+    double2 *P1 = p.ws + (long)wave * WAVE * WS_G, *Le2 = P1 + (long)rows_of(N) * rs, *Le1 = Le2 + (long)rows_of(N) * rs;
     const int nw = (N + WIN_MIN - 1) / WIN_MIN;
-    float4 *ck = p.ck + (long)wave * WAVE;
+    float4 *ck = p.ck + (long)wave * WAVE * WS_G;
     float4 *ring = ck + (long)nw * 4 * rs;
+    double2 *sink = p.aux + WAVE + (long)wave * WAVE;
     int buf = 0;
     pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
     pro.publish();
@@ -1046,8 +1099,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : nullptr, inv, lane, rs},
-                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs, p.p1_used}, N, ck, ring, rs, lane, sf,
+            run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
+                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
                                 lv, ll);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf,
@@ -1070,8 +1123,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             for (int kk = 0; kk < kn; ++kk) {
                 const int k = kc + kk;
                 const float4 x = at(X, k * WAVE + lane);
-                const double2 la = at(Le2, inv[k] * rs + lane);
-                const double2 le = at(Le1, k * rs + lane);
+                const double2 la = at(Le2, wsrow(inv[k], rs) + lane);
+                const double2 le = at(Le1, wsrow(k, rs) + lane);
                 const double fa = ((double)x.x + la.x) + le.x;
                 const double fb = ((double)x.y + la.y) + le.y;
                 const uint32_t two = (fa < 0.0 ? 1u : 0u) | (fb < 0.0 ? 2u : 0u);
@@ -1108,8 +1161,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
             for (int k = 0; k < N; ++k) {
                 const float4 x = X[(long)k * WAVE + lane];
-                const double2 la = Le2[(long)inv[k] * rs + lane];
-                const double2 le = Le1[(long)k * rs + lane];
+                const double2 la = Le2[wsrow(inv[k], rs) + lane];
+                const double2 le = Le1[wsrow(k, rs) + lane];
                 const double fa = ((double)x.x + la.x) + le.x;
                 const double fb = ((double)x.y + la.y) + le.y;
                 *reinterpret_cast<int2 *>(bo + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
@@ -1131,20 +1184,20 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 #endif
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
-    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
+    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ float4 lv[LDS_STAGE];
     __shared__ double2 ll[LDS_STAGE];
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
-    turbo_decode_tiles<0, RAG>(p, perm, inv, lv, ll, epi, PlanesIn{p.planes});
+    turbo_decode_tiles<0, RAG>(p, perm, inv, used, lv, ll, epi, PlanesIn{p.planes});
 }
 #ifndef TDEC_LM_WPE
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
 #endif
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
-    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv) {
+    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
-    turbo_decode_tiles<1, RAG>(p, perm, inv, nullptr, nullptr, epi, PlanesIn{p.planes});
+    turbo_decode_tiles<1, RAG>(p, perm, inv, used, nullptr, nullptr, epi, PlanesIn{p.planes});
 }
 
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).
@@ -1517,14 +1570,15 @@ template <typename T, int BPS> struct DemapPro {
 
 template <int ALGO, bool RAG, typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ALGO ? TDEC_LM_WPE : TDEC_ML_WPE))) void
-k_turbo_decode_syms(DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, FusedDemapArgs fa) {
+k_turbo_decode_syms(DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv,
+                    const int *__restrict__ used, FusedDemapArgs fa) {
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVES_PER_BLOCK * WAVE * DF_LD];
     load_table<T, BPS>(cons, reinterpret_cast<const T *>(fa.cons_g), fa.c);
     __syncthreads();
     DemapPro<T, BPS> pro{fa, p.B, cons, L + (threadIdx.x >> 6) * WAVE * DF_LD};
-    turbo_decode_tiles<ALGO, RAG>(p, perm, inv, nullptr, nullptr, epi, pro);
+    turbo_decode_tiles<ALGO, RAG>(p, perm, inv, used, nullptr, nullptr, epi, pro);
 }
 
 // ---- encoder (workload generation; encode, :404-462) ------------------------------

@@ -598,6 +598,14 @@ __device__ __forceinline__ bool lane_equal(const float (&x)[NS], const float4 *c
     return eq;
 }
 
+// Two state vectors are equal (IEEE ==, no short-circuit: one compare chain).
+__device__ __forceinline__ bool vec_equal(const float (&x)[NS], const float (&y)[NS]) {
+    bool eq = true;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) eq &= x[s] == y[s];
+    return eq;
+}
+
 template <bool ALPHA>
 __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base, int lane, const float (&x)[NS]) {
 #pragma unroll
@@ -619,10 +627,11 @@ __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base,
 // unconditional (the last window re-loads its own rows), so the number of
 // memory operations issued after them is the same on every path and the
 // compiler's wait counts stay exact.
-template <int ALGO, int W, bool RAG, class In, class Out>
+// B2 (CMP): `active` masks the stores of lanes that have merged.
+template <int ALGO, int W, bool RAG, bool CMP = false, class In, class Out>
 __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, int len, Raw (&raw)[W],
                                             float (&an)[NS], float (&b)[NS], const float4 *ck, unsigned cs, int lane,
-                                            int N, double sf) {
+                                            int N, double sf, bool active = true) {
     // len = steps in this window (W except for a ragged top window when W does not divide N)
     float gw[W][8], lcA[W], lcB[W];
     double iAw[W], iBw[W];
@@ -669,7 +678,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
         double leA, leB;
         extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
-        out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
+        if (!CMP || active) out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
         beta_step<ALGO>(b, gw[j]);
     }
 }
@@ -755,12 +764,69 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     bool merged = false;
-    for (int k0 = 0; k0 < N; k0 += W) {
-        if (TDEC_LANE_MERGE) {
+    // Two forms of the partial passes F2 / B2 (bit-identical):
+    //  masked:   a merged lane issues no loads or stores (fewer bytes; the branch
+    //            around them makes the compiler wait for every outstanding load)
+    //  unmasked: every lane loads (the inputs and the next compare vector one
+    //            group / window ahead, with exact wait counts); merged lanes
+    //            only skip their stores.
+    // Measured (round 2, 262 144 codewords): max-log masked 64.6 ms vs unmasked
+    // 66.7 (HBM-bound: bytes win), log-MAP masked 399.1 vs unmasked 393.0 ms.
+#ifndef TDEC_UNMASK_ML
+#define TDEC_UNMASK_ML 0
+#endif
+#ifndef TDEC_UNMASK_LM
+#define TDEC_UNMASK_LM 1
+#endif
+    constexpr bool UNMASK = ALGO ? TDEC_UNMASK_LM : TDEC_UNMASK_ML;
+    if (TDEC_LANE_MERGE && !UNMASK) {
+        for (int k0 = 0; k0 < N; k0 += W) {
             if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / W) * 4, lane);
             if (__all(merged)) break;
-        } else if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
-        if (!merged) {
+            if (!merged) {
+                float g[W][8];
+#pragma unroll
+                for (int j = 0; j < W; ++j) {
+                    double iA, iB;
+                    in.gamma(raw[j], g[j], iA, iB);
+                }
+                if (k0 + W < N) {
+#pragma unroll
+                    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
+                }
+                store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
+#pragma unroll
+                for (int j = 0; j < W; ++j)
+                    if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
+            }
+        }
+    } else if (TDEC_LANE_MERGE) {
+        // The checkpoint each group compares against is loaded one group ahead,
+        // with the inputs, before the group's checkpoint store; all loads are
+        // unconditional, so no branch makes the compiler wait for them early.
+        float c[NS];
+        load_vec<true>(c, ck, cs, 0, lane);
+        for (int k0 = 0; k0 < N; k0 += W) {
+            if (!merged) merged = vec_equal(a, c);
+            if (__all(merged)) break;
+            float g[W][8];
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                double iA, iB;
+                in.gamma(raw[j], g[j], iA, iB);
+            }
+            const int kn = k0 + W < N ? k0 + W : k0;
+#pragma unroll
+            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(kn + j, N - 1) : kn + j);
+            load_vec<true>(c, ck, cs, (kn / W) * 4, lane);
+            if (!merged) store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
+        }
+    } else {
+        for (int k0 = 0; k0 < N; k0 += W) {
+            if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
             float g[W][8];
 #pragma unroll
             for (int j = 0; j < W; ++j) {
@@ -797,12 +863,23 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     merged = false;
     for (int k0 = top; k0 >= 0; k0 -= W) {
         const int r = (top - k0) / W;
-        if (TDEC_LANE_MERGE) {
+        if (TDEC_LANE_MERGE && !UNMASK) {
             if (r % RSTEP == 0 && r < RING * RSTEP) {
                 if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP * 4, lane);
                 if (__all(merged)) break;
             }
             if (!merged) back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
+        } else if (TDEC_LANE_MERGE) {
+            // a merged lane keeps stepping (its later values equal beta1's) but
+            // stores nothing: its provisional extrinsics below are exact
+            if (r % RSTEP == 0 && r < RING * RSTEP) {
+                float rv[NS];
+                load_vec<false>(rv, ring, cs, r / RSTEP * 4, lane);
+                if (!merged) merged = vec_equal(b, rv);
+                if (__all(merged)) break;
+            }
+            back_window<ALGO, W, RAG, true>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf,
+                                            !merged);
         } else {
             if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
             back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);

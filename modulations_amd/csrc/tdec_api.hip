@@ -931,7 +931,7 @@ int tdec_reserve_fused(tdec_t *h, int max_batch) {
 }
 
 int tdec_fused_available(const tdec_t *h, int cons_f64, int bps) {
-    return h && fused_kernel(h->algo, h->N % win_of(h->algo) != 0, cons_f64 != 0, bps) != nullptr;
+    return h && fused_kernel(h->algo, h->N % win_unstaged(h->algo) != 0, cons_f64 != 0, bps) != nullptr;
 }
 
 int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
@@ -940,7 +940,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = check_demap_args(M, bps)) return rc;
     if (B == 0) return 0;
     if (!d_syms || !d_bits || S <= 0) return fail(TDEC_EINVAL, "bad demap-decode arguments");
-    const void *k = fused_kernel(h->algo, h->N % win_of(h->algo) != 0, cons_f64 != 0, bps);
+    const void *k = fused_kernel(h->algo, h->N % win_unstaged(h->algo) != 0, cons_f64 != 0, bps);
     if (!k) return fail(TDEC_EUNSUPPORTED, "no fused demap-decode kernel for this modulation / algorithm");
     Guard g(h->device);
     const int tiles = n_tiles_of(B), waves = waves_for(h, B);

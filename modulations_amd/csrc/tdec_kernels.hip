@@ -390,30 +390,53 @@ struct Raw {
 };
 
 // ---- LDS-DMA staging (siso8) ----------------------------------------------------------
-// global_load_lds: the load writes LDS directly, lane l's bytes at base + l*size,
-// with no VGPR destination.
+// global_load_lds: the load writes LDS directly, lane l's bytes at M0 + l*size,
+// with no VGPR destination.  Issued by inline asm, not the builtin: the
+// compiler's wait-count pass cannot tell one LDS-DMA target from another, so
+// with the builtin it waits for every outstanding DMA (vmcnt(0)) before each
+// new one and before each LDS read, which defeats the double buffering.  The
+// asm DMA is invisible to that pass; the code waits for it explicitly
+// (wait_vm<n>) before reading what it wrote.  M0 is set here and used by nothing
+// else in these kernels (no builtin LDS DMA, no s_movrel, gfx9+ DS ops ignore it).
+// LDS pointers are kept in the LDS address space (32-bit offsets): generic
+// 64-bit pointers in the staging structs cost registers and were spilled.
 typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void glb_void;
-__device__ __forceinline__ void glds16(const void *g, void *l) {
-    __builtin_amdgcn_global_load_lds((glb_void *)g, (lds_void *)l, 16, 0, 0);
+typedef __attribute__((address_space(3))) float lds_f1;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) f4v lds_f4;
+typedef __attribute__((address_space(3))) d2v lds_d2;
+__device__ __forceinline__ float4 ld4(const lds_f4 *p) {
+    const f4v v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void glds4(const void *g, void *l) {
-    __builtin_amdgcn_global_load_lds((glb_void *)g, (lds_void *)l, 4, 0, 0);
+__device__ __forceinline__ double2 ld2(const lds_d2 *p) {
+    const d2v v = *p;
+    return make_double2(v.x, v.y);
 }
-// s_waitcnt vmcnt(8) (lgkmcnt / expcnt left open).  Vector-memory operations
-// retire in issue order, and at least 8 are issued after a window's LDS-DMA
-// (the 4 extrinsic stores of the bottom half and the 4 checkpoint loads of the
-// next window), so this retires the DMA without waiting for those stores.
-__device__ __forceinline__ void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70 | 8); }
-// s_waitcnt vmcnt(n) for the double-buffered staging: n = the LDS-DMA operations
-// of the NEXT window's stage (issued last), so everything older has retired.
-template <int n> __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70 | n); }
+__device__ __forceinline__ unsigned lds_addr(const lds_void *l) {
+    return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+}
+__device__ __forceinline__ void glds16(const void *g, lds_void *l) {
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr(l)), "v"(g) : "memory");
+}
+__device__ __forceinline__ void glds4(const void *g, lds_void *l) {
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_addr(l)), "v"(g) : "memory");
+}
+// s_waitcnt vmcnt(n) (lgkmcnt / expcnt left open): vector-memory operations
+// retire in issue order, so this retires everything but the last n issued.
+template <int n> __device__ __forceinline__ void wait_vm() {
+    static_assert(n >= 0 && n < 16, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory");
+}
+__device__ __forceinline__ void wait_vm_all() { wait_vm<8>(); }
 
 // A wave's staged half window: 4 steps x {16-B plane v, 16-B plane l} x 64 lanes.
 struct LdsStage {
-    float4 *v;
-    double2 *l;
+    lds_f4 *v;
+    lds_d2 *l;
     int lane;
+    lds_f4 *ck = nullptr;   // siso8: this wave's alpha-checkpoint slot [4][64] float4 (LDS-DMA)
 };
 
 // Decoder 1 in the tile layout: X = [N][64] float4 {A, B, W1, Y1} (uniform
@@ -443,8 +466,8 @@ struct TileIn {
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         Raw r;
-        r.v = st.v[j * WAVE + lane];
-        r.l = st.l[j * WAVE + lane];
+        r.v = ld4(st.v + j * WAVE + lane);
+        r.l = ld2(st.l + j * WAVE + lane);
         return r;
     }
     // retire all but the last stage's 4 x (X + La) DMA operations
@@ -475,16 +498,16 @@ struct TileInPre {
     // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         const float *z = reinterpret_cast<const float *>(&at(Z, k * WAVE + lane));
-        float *dst = reinterpret_cast<float *>(st.v + j * WAVE);
+        lds_f1 *dst = reinterpret_cast<lds_f1 *>(st.v + j * WAVE);
         glds4(z, dst);
         glds4(z + 1, dst + WAVE);
         glds16(&at(P, wsrow(p_idx[k], rs) + lane), st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
-        const float *zp = reinterpret_cast<const float *>(st.v + j * WAVE);
+        const lds_f1 *zp = reinterpret_cast<const lds_f1 *>(st.v + j * WAVE);
         Raw r;
         r.v = make_float4(0.0f, 0.0f, zp[lane], zp[WAVE + lane]);
-        r.l = st.l[j * WAVE + lane];
+        r.l = ld2(st.l + j * WAVE + lane);
         return r;
     }
     __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
@@ -929,43 +952,58 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
     }
 }
 
-// Window [k0, k0+len) of the backward sweep, len <= 8.  rt: this window's top
-// half inputs on entry, the next (lower) window's on exit.  st: this window's
-// bottom half on entry (LDS-DMA issued during the previous window), the next
-// window's in flight on exit.
-// Double-buffered staging (TDEC_STAGE_DB): the next window's bottom half is
-// issued into the other buffer at the START of this window, a whole window
-// ahead of its use, instead of after this window's last LDS read.
-#ifndef TDEC_STAGE_DB
-#define TDEC_STAGE_DB 1
-#endif
+// Window [k0, k0+len) of the backward sweep, len <= 8, in two halves of 4.
+// On entry rt holds this window's top-half inputs, an its alpha checkpoint and
+// st its bottom-half inputs (staged in LDS); on exit they hold the next (lower)
+// window's (st / sn swap with the window parity).  Every load is issued a
+// half window or more before its use and is unconditional (the last window
+// re-reads its own rows), so the compiler's wait counts stay exact:
+//   start:       top-half gammas from rt; DMA of the next bottom half into sn
+//   wait:        st and an have landed (issued a window / half window ago)
+//   top half:    alpha[k0+4] from the checkpoint over st; rt <- next top half
+//   bottom half: gammas from st; an <- next checkpoint
+// The window's checkpoint is DMA'd into the wave's LDS slot (st.ck) at the
+// previous window's bottom half, after that window's last read of the slot,
+// and read from it twice (alpha[k0+4] and the bottom half), so it holds no
+// registers across the top half.
+__device__ __forceinline__ void ck_stage(const float4 *ck, unsigned cs, unsigned base, int lane, lds_f4 *slot) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) glds16(&at(ck, (base + q) * cs + lane), slot + q * WAVE);
+}
+__device__ __forceinline__ void ck_read(const lds_f4 *slot, int lane, float (&x)[NS]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = ld4(slot + q * WAVE + lane);
+        x[vec_elem<true>(q, 0)] = v.x;
+        x[vec_elem<true>(q, 1)] = v.y;
+        x[vec_elem<true>(q, 2)] = v.z;
+        x[vec_elem<true>(q, 3)] = v.w;
+    }
+}
 template <int ALGO, bool RAG, class In, class Out>
 __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k0, int len, Raw (&rt)[4],
-                                             const LdsStage &st, const LdsStage &sn, float (&b)[NS],
-                                             const float4 *ck, unsigned cs, int lane, double sf) {
+                                             const LdsStage &st, const LdsStage &sn,
+                                             float (&b)[NS], const float4 *ck, unsigned cs, int lane, int N,
+                                             double sf) {
     const int lenT = RAG ? (len > 4 ? len - 4 : 0) : 4;
     const int lenB = RAG ? (len < 4 ? len : 4) : 4;
-    float a0[NS];
-    load_vec<true>(a0, ck, cs, (k0 / 8) * 4, lane);
-    if (TDEC_STAGE_DB && k0 > 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) in.stage(k0 - 8 + j, sn, j);
-    }
+    const int kn = k0 >= 8 ? k0 - 8 : 0;   // the next window
+    float gw[4][8], lcA[4], lcB[4];
+    double iAw[4], iBw[4];
     if (!RAG || lenT > 0) {
-        float gw[4][8], lcA[4], lcB[4];
-        double iAw[4], iBw[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             in.gamma(rt[j], gw[j], iAw[j], iBw[j]);
             lcA[j] = rt[j].v.x;
             lcB[j] = rt[j].v.y;
         }
-        // the staged bottom half (and the checkpoint) have landed
-        if (TDEC_STAGE_DB) in.wait_staged();
-        else wait_vm_all();
-        float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
+    }
 #pragma unroll
-        for (int s = 0; s < NS; ++s) a4[s] = a0[s];
+    for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
+    in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
+    if (!RAG || lenT > 0) {
+        float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
+        ck_read(st.ck, lane, a4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float g[8];
@@ -973,21 +1011,13 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             in.gamma(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
         }
-        if (k0 > 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) rt[j] = in.load(k0 - 4 + j);
-        }
+        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
         window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
     } else {
-        if (TDEC_STAGE_DB) in.wait_staged();
-        else wait_vm_all();
-        if (k0 > 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) rt[j] = in.load(k0 - 4 + j);
-        }
+        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
     }
-    float gw[4][8], lcA[4], lcB[4];
-    double iAw[4], iBw[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const Raw r = in.staged(st, j);
@@ -995,10 +1025,9 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
         lcA[j] = r.v.x;
         lcB[j] = r.v.y;
     }
-    if (!TDEC_STAGE_DB && k0 > 0) {   // the next window's bottom half, straight into LDS (the reads above are consumed)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) in.stage(k0 - 8 + j, st, j);
-    }
+    float a0[NS];
+    ck_read(st.ck, lane, a0);
+    ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);   // after the slot's last read (an earlier read returns the old bytes)
     window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
@@ -1053,6 +1082,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
             raw[j] = in.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
             in.stage(RAG ? min(top + j, N - 1) : top + j, lb, j);
         }
+        ck_stage(ck, cs, (top / CK) * 4, lane, lb.ck);
         merged = false;
         for (int k0 = top; k0 >= 0; k0 -= CK) {
             const int r = (top - k0) / CK;
@@ -1063,9 +1093,9 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
                 if (__all(merged)) break;
             }
             if (!merged) {
-                const bool odd = TDEC_STAGE_DB && (r & 1);
+                const bool odd = r & 1;
                 back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, odd ? lb1 : lb,
-                                        TDEC_STAGE_DB ? (odd ? lb : lb1) : lb, b, ck, cs, lane, sf);
+                                        odd ? lb : lb1, b, ck, cs, lane, N, sf);
             }
         }
     }
@@ -1079,14 +1109,14 @@ constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 #endif
 constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval of the row SISO (k_siso_batch)
 #ifndef TDEC_WIN_ML
-#define TDEC_WIN_ML 4
+#define TDEC_WIN_ML 8
 #endif
-// max-log checkpoint interval: 4 (siso<>), or 8 (siso8: LDS-DMA staged half
-// windows, bit-identical).  8 moves 12 % fewer bytes (1.33 vs 1.51 MB per
-// codeword, rocprof) but ran 5 % slower on MI355X (73.7 vs 69.8 ms per
-// 262 144 codewords, tools/ab.py): the extra serial alpha steps per window
-// expose latency that two waves per SIMD do not hide.  Kept as an A/B variant
-// (python -m modulations_amd.build --variant ml8 TDEC_WIN_ML=8).
+// max-log checkpoint interval of k_turbo_decode: 8 (siso8: LDS-DMA staged half
+// windows, bit-identical) or 4 (siso<>, build variant TDEC_WIN_ML=4).  8 moves
+// 13 % fewer bytes per codeword; it was slower (round 1: 73.7 vs 69.8 ms per
+// 262 144 codewords) until its loads were issued a half window or more ahead
+// with exact wait counts (inline-asm LDS DMA, checkpoint slot in LDS, 32-bit LDS
+// pointers): round 2, 62.4 vs 65.0 ms (tools/ab.py, same bits).
 constexpr int WIN_ML = TDEC_WIN_ML;
 #ifndef TDEC_WIN_LM
 #define TDEC_WIN_LM 2
@@ -1096,19 +1126,31 @@ __host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_
 // the workspace's checkpoint array is sized for the densest interval in use
 constexpr int WIN_MIN = WIN < WIN_ML ? (WIN < WIN_LM ? WIN : WIN_LM) : (WIN_ML < WIN_LM ? WIN_ML : WIN_LM);
 constexpr int LDS_STAGE1 = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
-constexpr int LDS_STAGE = LDS_STAGE1 * (TDEC_STAGE_DB ? 2 : 1);
+constexpr int LDS_STAGE = LDS_STAGE1 * 2;   // double-buffered (siso8)
+// siso8's LDS per block: lv = 2 staging buffers + the checkpoint slots (float4),
+// ll = 2 staging buffers (double2): 80 KiB, two blocks per CU.  The epilogue's
+// bit-packing words then live in the wave's own first staging slice (idle
+// between tiles) instead of a separate array that would not fit.
+constexpr int LDS_LV = LDS_STAGE + WAVES_PER_BLOCK * 4 * WAVE;
+constexpr int EPI_STRIDE_ML = TDEC_WIN_ML == 8 ? 4 * WAVE * 4 : 2 * WAVE;   // uint32 words between waves' epi areas
 
-// The SISO of the tile decoder: siso8 for max-log at WIN_ML 8, else siso<> at WIN.
-template <int ALGO, bool RAG, class In, class Out>
+// The SISO of the tile decoder: siso8 (LDS-staged, checkpoints every 8) for
+// max-log when the kernel provides the staging LDS (STAGED), else siso<> with
+// checkpoints every 4 (max-log, the fused demap-decode kernel) or WIN_LM.
+constexpr bool STAGED_ML = WIN_ML == 8;
+__host__ __device__ constexpr int win_unstaged(int algo) { return algo ? WIN_LM : 4; }
+template <int ALGO, bool RAG, bool STAGED, class In, class Out>
 __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs,
                                          int lane, double sf, float4 *lv, double2 *ll) {
-    if constexpr (ALGO == 0 && WIN_ML == 8) {
+    if constexpr (ALGO == 0 && STAGED) {
         const int w = threadIdx.x >> 6;
-        siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{lv + w * 4 * WAVE, ll + w * 4 * WAVE, lane},
-                         LdsStage{lv + (TDEC_STAGE_DB ? LDS_STAGE1 : 0) + w * 4 * WAVE,
-                                  ll + (TDEC_STAGE_DB ? LDS_STAGE1 : 0) + w * 4 * WAVE, lane});
+        lds_f4 *v = (lds_f4 *)lv;
+        lds_d2 *l = (lds_d2 *)ll;
+        lds_f4 *slot = v + LDS_STAGE + w * 4 * WAVE;
+        siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{v + w * 4 * WAVE, l + w * 4 * WAVE, lane, slot},
+                         LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot});
     } else {
-        siso<ALGO, (ALGO ? WIN_LM : WIN_ML), RAG>(in, out, N, ck, ring, cs, lane, sf);
+        siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
 }
 
@@ -1147,11 +1189,11 @@ struct PlanesIn {
     __device__ __forceinline__ void publish() const {}
 };
 
-template <int ALGO, bool RAG, class Pro = PlanesIn>
+template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, const int *__restrict__ used,
                                                    float4 *lv, double2 *ll,
-                                                   uint32_t *epi, const Pro &pro = Pro{}) {
+                                                   uint32_t *epi, const Pro &pro = Pro{}, int epi_stride = 2 * WAVE) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
@@ -1176,11 +1218,12 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            run_siso<ALGO, RAG>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
+            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
                                 lv, ll);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
-            run_siso<ALGO, RAG>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane, sf,
+            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
+                                        sf,
                                 lv, ll);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
@@ -1191,7 +1234,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         // writes the 64 rows chunk by chunk in row order (16-B int4 stores, each
         // wave store one contiguous 1 KiB run) instead of one 8-B store per lane
         // per couple 6 KB apart.
-        uint32_t *hb = epi + (threadIdx.x >> 6) * 2 * WAVE;
+        uint32_t *hb = epi + (threadIdx.x >> 6) * epi_stride;
         const long nb = 2L * N;
         for (int kc = 0; kc < N; kc += 32) {
             uint32_t w0 = 0, w1 = 0;
@@ -1262,10 +1305,15 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 template <bool RAG>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
-    __shared__ float4 lv[LDS_STAGE];
+    __shared__ float4 lv[LDS_LV];
     __shared__ double2 ll[LDS_STAGE];
-    __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
-    turbo_decode_tiles<0, RAG>(p, perm, inv, used, lv, ll, epi, PlanesIn{p.planes});
+    if constexpr (TDEC_WIN_ML == 8) {
+        turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
+                                   EPI_STRIDE_ML);
+    } else {
+        __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+        turbo_decode_tiles<0, RAG>(p, perm, inv, used, lv, ll, epi, PlanesIn{p.planes});
+    }
 }
 #ifndef TDEC_LM_WPE
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)

@@ -513,6 +513,20 @@ struct TileInPre {
     __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
 };
 
+// Workspace stores (extrinsic planes, checkpoints): nothing re-reads them before
+// L2 would have evicted them, so TDEC_NT_STORE marks them non-temporal.
+#ifndef TDEC_NT_STORE
+#define TDEC_NT_STORE 0
+#endif
+__device__ __forceinline__ void ws_store(double2 &dst, const double2 &v) {
+    if (TDEC_NT_STORE) __builtin_nontemporal_store((d2v){v.x, v.y}, reinterpret_cast<d2v *>(&dst));
+    else dst = v;
+}
+__device__ __forceinline__ void ws_store(float4 &dst, const float4 &v) {
+    if (TDEC_NT_STORE) __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(&dst));
+    else dst = v;
+}
+
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
 // iteration) Le1 itself for the final decision (:529-530).
 // P1[k] is read by decoder 2 only as P1[perm[k']]: perm is not a permutation
@@ -535,8 +549,8 @@ struct TileOutPre {
         // wave-uniform row selects (SGPR pairs), then the lane offset
         double2 *rp = (TDEC_P1_ALL || used[k]) ? &at(P, wsrow(k, rs)) : sink;
         double2 *rl = Le ? &at(Le, wsrow(k, rs)) : sink;
-        at(rp, (unsigned)lane) = make_double2((double)lcA + a, (double)lcB + b);
-        at(rl, (unsigned)lane) = make_double2(a, b);
+        ws_store(at(rp, (unsigned)lane), make_double2((double)lcA + a, (double)lcB + b));
+        ws_store(at(rl, (unsigned)lane), make_double2(a, b));
     }
 };
 
@@ -545,7 +559,7 @@ struct TileOut {
     int lane;
     unsigned rs;
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
-        at(Le, wsrow(k, rs) + lane) = make_double2(a, b);
+        ws_store(at(Le, wsrow(k, rs) + lane), make_double2(a, b));
     }
 };
 
@@ -633,8 +647,8 @@ template <bool ALPHA>
 __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base, int lane, const float (&x)[NS]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        at(c, (base + q) * cs + lane) = make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
-                                                      x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]);
+        ws_store(at(c, (base + q) * cs + lane), make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
+                                                            x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]));
 }
 
 // Window of the backward sweep fused with the extrinsic (:220-281): steps
@@ -935,7 +949,10 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
         if (RAG && j >= len) continue;       // wave-uniform
-        __builtin_amdgcn_sched_barrier(0);
+#ifndef TDEC_HALF_SB
+#define TDEC_HALF_SB 1
+#endif
+        if (TDEC_HALF_SB) __builtin_amdgcn_sched_barrier(0);
         const int from = j >= H ? H : 0;
         float aj[NS];
 #pragma unroll

@@ -377,6 +377,19 @@ void tdec_destroy(tdec_t *h) {
     Guard g(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->pending) hipEventSynchronize(h->done_ev);
+#if TDEC_PASS_TIMING
+    {   // measurement build: per-pass cycles of every decode since the last destroy
+        unsigned long long c[8] = {};
+        hipDeviceSynchronize();
+        if (hipMemcpyFromSymbol(c, HIP_SYMBOL(g_pass_cycles), sizeof(c)) == hipSuccess) {
+            const double t = (double)(c[0] + c[1] + c[2] + c[3] + c[4]);
+            fprintf(stderr, "[tdec] pass cycles: F1 %.3f F2 %.3f B1 %.3f B2 %.3f epilogue %.3f (total %.3e)\n",
+                    c[0] / t, c[1] / t, c[2] / t, c[3] / t, c[4] / t, t);
+            const unsigned long long z[8] = {};
+            hipMemcpyToSymbol(HIP_SYMBOL(g_pass_cycles), z, sizeof(z));
+        }
+    }
+#endif
     hipFree(h->d_perm);
     hipFree(h->d_used);
     hipFree(h->d_inv);

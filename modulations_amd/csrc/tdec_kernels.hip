@@ -1050,9 +1050,27 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
 
 constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16-step grid over the top 256 steps
 
+// TDEC_PASS_TIMING (measurement build): per-pass shader-clock cycles summed
+// over all waves (s_memtime, one vector atomic from lane 0 per pass), printed
+// by tdec_destroy: [0] F1, [1] F2, [2] B1, [3] B2, [4] epilogue.
+#ifndef TDEC_PASS_TIMING
+#define TDEC_PASS_TIMING 0
+#endif
+#if TDEC_PASS_TIMING
+__device__ unsigned long long g_pass_cycles[8];
+__device__ __forceinline__ void pass_mark(unsigned long long &t, int slot) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&g_pass_cycles[slot], now - t);
+    t = now;
+}
+#else
+__device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
+#endif
+
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
                       const LdsStage &lb, const LdsStage &lb1) {
+    unsigned long long tpass = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
     constexpr int G = 4, CK = 8;
     const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
     Raw raw[G];
@@ -1061,7 +1079,11 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
     // F1: inputs pipelined one group of FG steps ahead, checkpoint every 8
     f1_pass<ALGO, CK, RAG>(in, N, ck, cs, lane, a);
-    // F2 until merged with F1 at a checkpoint
+    pass_mark(tpass, 0);
+    // F2 until merged with F1 at a checkpoint.  (Measured alternative, round 2:
+    // the next checkpoint prefetched one interval ahead with unmasked input
+    // loads cut F2's share of wave time from 7.4 to 5.6 % but the extra bytes
+    // made the decode 1.1 % slower.)
 #pragma unroll
     for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     bool merged = false;   // per lane, as siso<>
@@ -1088,6 +1110,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
                 if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
     }
+    pass_mark(tpass, 1);
     // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
     float b[NS];
 #pragma unroll
@@ -1115,6 +1138,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
                                         odd ? lb : lb1, b, ck, cs, lane, N, sf);
             }
         }
+        pass_mark(tpass, 2 + pass);
     }
 }
 
@@ -1244,6 +1268,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                                 lv, ll);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
+        unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
         const long cw = (long)tile * WAVE + lane;
 #if TDEC_EPI_LDS
@@ -1307,6 +1332,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             }
         }
 #endif
+        pass_mark(tepi, 4);
         if (has_next) pro.publish();
         buf ^= 1;
     }

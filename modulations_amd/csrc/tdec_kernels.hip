@@ -749,7 +749,13 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 #endif
 template <int ALGO, int W, bool RAG, class In>
 __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigned cs, int lane, float (&a)[NS]) {
-    constexpr int FG = TDEC_FG > W ? TDEC_FG : W;   // a multiple of W
+    // log-MAP: one checkpoint interval per group (its steps are ~10x larger, and
+    // the kernel's instruction footprint, not load latency, is what costs)
+#ifndef TDEC_FG_LM
+#define TDEC_FG_LM 2
+#endif
+    constexpr int FGW = ALGO ? TDEC_FG_LM : TDEC_FG;
+    constexpr int FG = FGW > W ? FGW : W;   // a multiple of W
     static_assert(FG % W == 0, "FG must be a multiple of W");
     // steps past N exist only when W does not divide N (RAG) or FG > W
     const bool tail = RAG || (FG > W && N % FG != 0);
@@ -777,6 +783,15 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
     }
 }
 
+#ifndef TDEC_UNMASK_ML
+#define TDEC_UNMASK_ML 0
+#endif
+#ifndef TDEC_UNMASK_LM
+#define TDEC_UNMASK_LM 1
+#endif
+#ifndef TDEC_LANE_MERGE
+#define TDEC_LANE_MERGE 1
+#endif
 constexpr int RING = 16;   // beta1 kept at RING window starts 16 steps apart: the top 256 steps (merge: median 40, max 122)
 __host__ __device__ constexpr int rstep_of(int w) { return w >= 16 ? 1 : 16 / w; }
 
@@ -789,15 +804,13 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
+    constexpr bool UNMASK = ALGO ? TDEC_UNMASK_LM : TDEC_UNMASK_ML;
     // F1 (inputs software-pipelined one group of FG steps ahead)
     f1_pass<ALGO, W, RAG>(in, N, ck, cs, lane, a);
     // F2 until merged (a = alpha1[N] = alpha2[0]).  Per lane: once alpha2 ==
     // alpha1 at a checkpoint, every later checkpoint already holds alpha2, so
     // the lane stops loading and storing (masked lanes move no bytes); the
     // wave runs until every lane has merged.
-#ifndef TDEC_LANE_MERGE
-#define TDEC_LANE_MERGE 1
-#endif
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     bool merged = false;
@@ -809,13 +822,6 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     //            only skip their stores.
     // Measured (round 2, 262 144 codewords): max-log masked 64.6 ms vs unmasked
     // 66.7 (HBM-bound: bytes win), log-MAP masked 399.1 vs unmasked 393.0 ms.
-#ifndef TDEC_UNMASK_ML
-#define TDEC_UNMASK_ML 0
-#endif
-#ifndef TDEC_UNMASK_LM
-#define TDEC_UNMASK_LM 1
-#endif
-    constexpr bool UNMASK = ALGO ? TDEC_UNMASK_LM : TDEC_UNMASK_ML;
     if (TDEC_LANE_MERGE && !UNMASK) {
         for (int k0 = 0; k0 < N; k0 += W) {
             if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / W) * 4, lane);
@@ -841,6 +847,8 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
         // The checkpoint each group compares against is loaded one group ahead,
         // with the inputs, before the group's checkpoint store; all loads are
         // unconditional, so no branch makes the compiler wait for them early.
+        // (Running F1 as pass 0 of this loop, one copy of the code, measured no
+        // faster: 385.3 vs 381.1 ms per 262 144 log-MAP codewords.)
         float c[NS];
         load_vec<true>(c, ck, cs, 0, lane);
         for (int k0 = 0; k0 < N; k0 += W) {
@@ -880,49 +888,47 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
                 if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
     }
-    // B1 fused with the provisional extrinsic
+    // B1 fused with the provisional extrinsic, then B2 until merged (b =
+    // beta1[0] = beta2[N]); per lane as F2: below its merge point a lane's
+    // provisional extrinsics are exact, it stops there.  One copy of the window
+    // code serves both passes (the pass loop is not unrolled: the kernels'
+    // instruction footprint, see siso8).
     float b[NS], an[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
-    load_vec<true>(an, ck, cs, (top / W) * 4, lane);
-    for (int k0 = top; k0 >= 0; k0 -= W) {
-        const int r = (top - k0) / W;                     // window index from the top
-        if (r % RSTEP == 0 && r < RING * RSTEP) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
-        back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
-    }
-    // B2 until merged (b = beta1[0] = beta2[N]); per lane as F2: below its
-    // merge point a lane's provisional extrinsics are exact, it stops there
-#pragma unroll
-    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
-    load_vec<true>(an, ck, cs, (top / W) * 4, lane);
-    merged = false;
-    for (int k0 = top; k0 >= 0; k0 -= W) {
-        const int r = (top - k0) / W;
-        if (TDEC_LANE_MERGE && !UNMASK) {
-            if (r % RSTEP == 0 && r < RING * RSTEP) {
-                if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP * 4, lane);
-                if (__all(merged)) break;
+        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+        load_vec<true>(an, ck, cs, (top / W) * 4, lane);
+        merged = false;
+        for (int k0 = top; k0 >= 0; k0 -= W) {
+            const int r = (top - k0) / W;                     // window index from the top
+            const bool keep = r % RSTEP == 0 && r < RING * RSTEP;
+            if (pass == 0) {
+                if (keep) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
+            } else if (keep) {
+                if (TDEC_LANE_MERGE) {
+                    float rv[NS];
+                    load_vec<false>(rv, ring, cs, r / RSTEP * 4, lane);
+                    if (!merged) merged = vec_equal(b, rv);
+                    if (__all(merged)) break;
+                } else if (wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) {
+                    break;
+                }
             }
-            if (!merged) back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
-        } else if (TDEC_LANE_MERGE) {
-            // a merged lane keeps stepping (its later values equal beta1's) but
-            // stores nothing: its provisional extrinsics below are exact
-            if (r % RSTEP == 0 && r < RING * RSTEP) {
-                float rv[NS];
-                load_vec<false>(rv, ring, cs, r / RSTEP * 4, lane);
-                if (!merged) merged = vec_equal(b, rv);
-                if (__all(merged)) break;
+            if (UNMASK) {
+                // a merged lane keeps stepping (its later values equal beta1's) but
+                // stores nothing
+                back_window<ALGO, W, RAG, true>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N,
+                                                sf, !merged);
+            } else if (!merged) {
+                back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
             }
-            back_window<ALGO, W, RAG, true>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf,
-                                            !merged);
-        } else {
-            if (r % RSTEP == 0 && r < RING * RSTEP && wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) break;
-            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
         }
     }
 }
+
 
 // ---- max-log SISO with alpha checkpoints every 8 steps ---------------------------
 // Halves the checkpoint stream of siso<> (16 B per step -> 8 B written, and the
@@ -1115,7 +1121,19 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
     float b[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
+    // TDEC_B_ONECOPY: B1 and B2 share one copy of the window code (the pass
+    // loop is not unrolled), halving the backward sweep's instruction footprint:
+    // the kernel shrinks from 15.2 k to 9.6 k instructions and decodes 1.5 %
+    // faster (62.6 -> 61.7 ms per 262 144 codewords, same bits): the waves of a
+    // CU run different passes at once and share its instruction cache.
+#ifndef TDEC_B_ONECOPY
+#define TDEC_B_ONECOPY 1
+#endif
+#if TDEC_B_ONECOPY
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

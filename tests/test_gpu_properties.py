@@ -104,3 +104,28 @@ def test_reference_interleaver_error_floor_is_deterministic():
     assert errs.min() > 0
     sample = [0, 4500, 8999]
     assert np.array_equal(bits[sample].cpu().numpy(), _oracle_bits(codec, llr[sample].cpu().numpy()))
+
+
+@pytest.mark.parametrize("n,mod", [(212, "QPSK"), (220, "16QAM")])
+def test_ragged_checkpoint_windows_full_size(n, mod):
+    """N not a multiple of the max-log decoder's 8-step checkpoint interval
+    (ragged top window in siso8), a batch past the resident-wave count (the
+    persistent tile loop wraps) and not a multiple of 64: deterministic, and the
+    first / middle / last codewords equal the oracle's."""
+    dev = torch.device("cuda", 0)
+    codec = M.DVBRCS2_Turbo(n, "1/3")
+    assert codec.N % 8 != 0
+    B = 140_001
+    _, syms, n0 = make_symbols(codec, B, mod, 1.5, 21, dev, want_info=False)
+    pipe = DevicePipeline(codec, mod, B, dev)
+    b1 = pipe.run(syms, n0).clone()
+    b2 = pipe.run(syms, n0).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(b1, b2)
+    cons = D.constellation(mod)
+    bps = D.MODULATIONS[mod]["bps"]
+    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
+    idx = [0, 64, 131_071, 131_072, B // 2, B - 1]
+    rows = syms[idx].cpu().numpy()
+    llr = np.stack([-O.demap(r, cons, bps, nve, div_f32=div32)[:codec.n_coded] for r in rows]).astype(np.float32)
+    assert np.array_equal(b1[idx].cpu().numpy(), _oracle_bits(codec, llr))

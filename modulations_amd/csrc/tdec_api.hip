@@ -212,6 +212,7 @@ struct tdec_ctx {
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
+    int *d_tile_ctr = nullptr;         // the decoders' tile queue counter (zeroed before each launch)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
     int row_pad = 0;   // TDEC_ROW_PAD (placement study): lanes of padding per workspace row
@@ -340,6 +341,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMemcpy(h->d_used, used.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
+    if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
     if (e == hipSuccess) e = hipMemcpy(h->d_off, off.data(), sizeof(int32_t) * (N + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_perm, perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
@@ -394,6 +396,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_used);
     hipFree(h->d_inv);
     hipFree(h->d_src);
+    hipFree(h->d_tile_ctr);
     hipFree(h->d_off);
     h->ws.release();
     h->planes_own.release();
@@ -424,6 +427,24 @@ static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 // Per-wave workspace strides (elements).
 static long ws_stride_of(const tdec_t *h) { return 3L * rows_of(h->N) * WAVE; }
 static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) / WIN_MIN + RING) * 4 * WAVE; }
+
+// The decoders' tile queue: the counter zeroed on the launch's stream, or null
+// (static striding) below 4 tiles per wave or with TDEC_DYN_TILES=0.  Measured
+// (same bits): 1 M codewords (8 tiles per wave) 243.8 -> 241.6 ms; at 2 tiles
+// per wave the queue was no faster (max-log 61.8 vs 62.6, log-MAP 381.2 vs
+// 385.9 ms per 262 144), hence the threshold.
+static int *tile_queue(tdec_t *h, int tiles, int waves, hipStream_t st) {
+#ifndef TDEC_DYN_DEFAULT
+#define TDEC_DYN_DEFAULT 1
+#endif
+    static const bool dyn = [] {
+        const char *e = getenv("TDEC_DYN_TILES");
+        return e ? e[0] != '0' : TDEC_DYN_DEFAULT != 0;
+    }();
+    if (!dyn || tiles < 4 * waves) return nullptr;
+    if (hipMemsetAsync(h->d_tile_ctr, 0, sizeof(int), st) != hipSuccess) return nullptr;
+    return h->d_tile_ctr;
+}
 
 // Time one single-iteration decode of waves*64 codewords of constant LLRs on a
 // candidate workspace (the placement probe below).
@@ -591,12 +612,12 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
-                 h->aux_p};
-    const int *pm = h->d_perm, *iv = h->d_inv;
-    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
+                 h->aux_p, tile_queue(h, tiles, waves, st)};
+    const int *pm = h->d_perm, *iv = h->d_inv;
+    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, st,
                        a, pm, iv, (const int *)h->d_used);
     HIPCHK(hipGetLastError());
@@ -963,7 +984,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
-                 h->aux_p};
+                 h->aux_p, tile_queue(h, tiles, waves, st)};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};

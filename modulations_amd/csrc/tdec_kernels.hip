@@ -1229,6 +1229,7 @@ struct DecodeArgs {
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
     int row_pad;             // lanes of padding after each workspace row (0 unless TDEC_ROW_PAD)
     double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
+    int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1268,11 +1269,20 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     int buf = 0;
     pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
     pro.publish();
-    for (int tile = wave; tile < p.n_tiles; tile += p.n_waves) {
+    // Every wave starts with tile `wave`; with a tile counter the next tile is
+    // taken from a queue (one atomic per tile from lane 0, issued at the tile's
+    // start, consumed at its end), so waves whose codewords take longer (longer
+    // merge passes) take fewer tiles and all waves finish close together.
+    for (int tile = wave; tile < p.n_tiles;) {
         const float *base = pro.tile_planes(tile, wave, N, buf);
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
-        const int nxt = tile + p.n_waves;
+        int nxt = tile + p.n_waves;
+        if (p.tile_ctr) {
+            int q = 0;
+            if (lane == 0) q = atomicAdd(p.tile_ctr, 1);
+            nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
+        }
         const bool has_next = nxt < p.n_tiles;
         for (int it = 0; it < p.iters; ++it) {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
@@ -1353,6 +1363,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         pass_mark(tepi, 4);
         if (has_next) pro.publish();
         buf ^= 1;
+        tile = nxt;
     }
 }
 

@@ -616,21 +616,24 @@ __device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 v = at(c, (base + q) * cs + lane);
-        eq = eq && x[vec_elem<ALPHA>(q, 0)] == v.x && x[vec_elem<ALPHA>(q, 1)] == v.y &&
-             x[vec_elem<ALPHA>(q, 2)] == v.z && x[vec_elem<ALPHA>(q, 3)] == v.w;
+        eq &= (x[vec_elem<ALPHA>(q, 0)] == v.x) & (x[vec_elem<ALPHA>(q, 1)] == v.y) &
+              (x[vec_elem<ALPHA>(q, 2)] == v.z) & (x[vec_elem<ALPHA>(q, 3)] == v.w);
     }
     return __all(eq);
 }
 
-// This lane's vector equals the stored one (IEEE ==).
+// This lane's vector equals the stored one (IEEE ==).  No short-circuit: with
+// `&&` the compiler issued the four loads one after another, each behind the
+// previous compare (four round trips per merge check instead of one; measured
+// the same speed, r02ap_nsc.log: the other wave hides them).
 template <bool ALPHA>
 __device__ __forceinline__ bool lane_equal(const float (&x)[NS], const float4 *c, unsigned cs, unsigned base, int lane) {
     bool eq = true;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 v = at(c, (base + q) * cs + lane);
-        eq = eq && x[vec_elem<ALPHA>(q, 0)] == v.x && x[vec_elem<ALPHA>(q, 1)] == v.y &&
-             x[vec_elem<ALPHA>(q, 2)] == v.z && x[vec_elem<ALPHA>(q, 3)] == v.w;
+        eq &= (x[vec_elem<ALPHA>(q, 0)] == v.x) & (x[vec_elem<ALPHA>(q, 1)] == v.y) &
+              (x[vec_elem<ALPHA>(q, 2)] == v.z) & (x[vec_elem<ALPHA>(q, 3)] == v.w);
     }
     return eq;
 }
@@ -1478,11 +1481,129 @@ template <typename T> __device__ __forceinline__ double llr_of(T lo, T hi, const
     return c.sign < 0 ? -v : v;
 }
 
+// Square QAM whose label splits into K I-bits and K Q-bits (16/64/256QAM of
+// sdr_modem.py:142-220): point (a, q) = levI[a] + j levQ[q].  The minimum of
+// numpy's |s - c|^2 over a bit-half is taken at the point nearest in plain
+// dx^2 + dy^2 (computed from the same rounded differences) unless two points of
+// the half are within a relative 64 ulp of each other: that point is found per
+// axis (2^K levels instead of 2^(2K) points) and only the 2*BPS candidates get
+// numpy's distance.  Near ties, non-finite input or underflow return false and
+// the caller runs the full scan, so the result is the scan's, bit for bit.
+//
+// The gap test may be stricter than needed, never looser (a stricter test only
+// sends more symbols to the exact scan): one tolerance from the largest
+// candidate distance serves every half, and once every gap is strictly positive
+// the argmin of a half is unique, so min / max order statistics and any
+// tie-break give the same candidates.  Inside the fast path every difference is
+// finite, so |z| skips numpy's inf / NaN rules (cabs_fin).
+// numpy's |z| (npm::cabs_np) for finite re, im: the same operations without the
+// inf / NaN selects; f32's square root of fma(r, r, 1) in [1, 2] as the raw
+// v_sqrt_f32 plus the compiler's own +-1 ulp correction (its input scaling and
+// zero / inf class test are identities on [1, 2]), so bit-identical to sqrtf.
+template <typename T> __device__ __forceinline__ T sqrt_1_2(T x) {
+    if constexpr (sizeof(T) == 8) {
+        return sqrt(x);
+    } else {
+        const float r = __builtin_amdgcn_sqrtf(x);
+        const float dn = __int_as_float(__float_as_int(r) - 1), up = __int_as_float(__float_as_int(r) + 1);
+        const float rd = __builtin_fmaf(-dn, r, x), ru = __builtin_fmaf(-up, r, x);
+        const float t = rd <= 0.0f ? dn : r;
+        return ru > 0.0f ? up : t;
+    }
+}
+template <typename T> __device__ __forceinline__ T cabs_fin(T re, T im) {
+    re = fabs(re);
+    im = fabs(im);
+    const T larger = re > im ? re : im;
+    const T smaller = im < re ? im : re;
+    const T ratio = larger != (T)0 ? smaller / larger : (T)0;
+    return sqrt_1_2<T>(fma(ratio, ratio, (T)1)) * larger;
+}
+
+template <typename T, int BPS>
+__device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    constexpr int K = BPS / 2, L = 1 << K;
+    const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
+    const T inf = (T)INFINITY;
+    const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
+    T all1[2], all2[2], b1[2][K][2], b2[2][K][2];   // nearest / second nearest: axis, bit-halves
+    int arg[2][K][2], allarg[2];
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        const T s = ax ? si : sr;
+        const T *lev = ax ? lev_q : lev_i;
+        // streamed over the levels: nearest / second nearest of the axis and of
+        // each bit-half (a NaN distance is dropped by fmin / fmax; then every
+        // distance of the axis is NaN, the minima stay inf and the test below
+        // fails)
+        T m1 = inf, m2 = inf;
+        int am = 0;
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                b1[ax][b][v] = b2[ax][b][v] = inf;
+                arg[ax][b][v] = 0;
+            }
+#pragma unroll
+        for (int a = 0; a < L; ++a) {
+            const T d = s - lev[a];
+            const T d2 = d * d;
+            m2 = fmin(m2, fmax(m1, d2));
+            am = d2 < m1 ? a : am;
+            m1 = fmin(m1, d2);
+#pragma unroll
+            for (int b = 0; b < K; ++b) {
+                const int v = (a >> (K - 1 - b)) & 1;
+                b2[ax][b][v] = fmin(b2[ax][b][v], fmax(b1[ax][b][v], d2));
+                arg[ax][b][v] = d2 < b1[ax][b][v] ? a : arg[ax][b][v];
+                b1[ax][b][v] = fmin(b1[ax][b][v], d2);
+            }
+        }
+        all1[ax] = m1;
+        all2[ax] = m2;
+        allarg[ax] = am;
+    }
+    T gap = fmin(all2[0] - all1[0], all2[1] - all1[1]), top = (T)0, hi = fmax(all2[0], all2[1]);
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax)
+#pragma unroll
+        for (int b = 0; b < K; ++b)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                gap = fmin(gap, b2[ax][b][v] - b1[ax][b][v]);
+                top = fmax(top, b1[ax][b][v]);
+                hi = fmax(hi, b2[ax][b][v]);
+            }
+    // every gap above the tolerance of the largest candidate distance
+    // (best + the other axis' nearest), every second nearest finite
+    const T tol = eps * (top + fmax(all1[0], all1[1])) + tau;
+    if (!(hi < inf && gap > tol)) return false;
+    // The half holding the overall nearest point has that point as its
+    // candidate, so its distance is shared by every bit: BPS + 1 numpy
+    // distances instead of 2 * BPS.
+    const T an = cabs_fin<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
+    const T dn = an * an;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax)
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
+            const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
+            const T a = cabs_fin<T>(sr - lev_i[ia], si - lev_q[iq]);
+            T m[2];
+            m[vn] = dn;
+            m[vo] = a * a;
+            out[ax * K + b] = llr_of<T>(m[0], m[1], c);
+        }
+    return true;
+}
+
 // All BPS LLRs of one symbol, reference sign (positive -> bit 1) unless
 // c.sign < 0.  Streams over the M points keeping a running min per bit and
 // label value, so no distance array is materialised.
-template <typename T, int BPS, int M = (1 << BPS)>
-__device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+template <typename T, int BPS, bool FIN, int M = (1 << BPS)>
+__device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     T m0[BPS], m1[BPS];
     bool n0[BPS], n1[BPS];
 #pragma unroll
@@ -1494,7 +1615,7 @@ __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapC
 #pragma unroll (M <= 16 ? M : 8)
     for (int m = 0; m < M; ++m) {
         if (M > 2 && m >= c.M) break;
-        const T a = cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
+        const T a = FIN ? cabs_fin<T>(sr - cons[2 * m], si - cons[2 * m + 1]) : cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
         const T v = a * a;                     // np.abs(s - constellation) ** 2
         const bool vn = v != v;
 #pragma unroll
@@ -1513,16 +1634,26 @@ __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapC
         out[b] = llr_of<T>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
 }
 
-// Square QAM whose label splits into K I-bits and K Q-bits (16/64/256QAM of
-// sdr_modem.py:142-220): point (a, q) = levI[a] + j levQ[q].  The minimum of
-// numpy's |s - c|^2 over a bit-half is taken at the point nearest in plain
-// dx^2 + dy^2 (computed from the same rounded differences) unless two points of
-// the half are within a relative 64 ulp of each other: that point is found per
-// axis (2^K levels instead of 2^(2K) points) and only the 2*BPS candidates get
-// numpy's distance.  Near ties, non-finite input or underflow return false and
-// the caller runs the full scan, so the result is the scan's, bit for bit.
+// With every lane's symbol finite (the table is), every difference is finite
+// and |z| is cabs_fin; BPSK / QPSK / 8PSK (M <= 8, the scan is their only
+// path) take that copy when the whole wave qualifies.
+template <typename T, int BPS, int M = (1 << BPS)>
+__device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    if constexpr (M <= 8) {
+        if (__all(isfinite(sr) && isfinite(si))) {
+            sym_llrs_scan<T, BPS, true>(sr, si, cons, c, out);
+            return;
+        }
+    }
+    sym_llrs_scan<T, BPS, false>(sr, si, cons, c, out);
+}
+
+// 256QAM (K = 4) keeps the previous form of the same search (per-half best and
+// second by compare-select, numpy's |z| with its inf / NaN rules): the form
+// above compiles to 198-230 VGPRs at K = 4 (2 waves per SIMD, 70.6 -> 100.8 ms
+// per 1 M codewords) against 135; at K = 2 / 3 it is 12 % faster.
 template <typename T, int BPS>
-__device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+__device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr int K = BPS / 2, L = 1 << K;
     const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
     const T inf = (T)INFINITY;
@@ -1594,8 +1725,11 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
 
 template <typename T, int BPS>
 __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
-    if constexpr (BPS >= 4 && BPS % 2 == 0)
+    if constexpr (BPS >= 8 && BPS % 2 == 0) {
+        if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return;
+    } else if constexpr (BPS >= 4 && BPS % 2 == 0) {
         if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return;
+    }
     sym_llrs<T, BPS>(sr, si, cons, c, out);
 }
 
@@ -1648,8 +1782,15 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
     const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
     const int ns = (int)(s1 - s0);
     __syncthreads();
-    for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK) {
-        const int lane = t / ns, si = t % ns;                    // consecutive threads: consecutive symbols
+    // item t = (lane, si), consecutive threads: consecutive symbols; the
+    // quotient and remainder of t by ns advance by those of BLOCK each step
+    const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
+    int lane = (int)threadIdx.x / ns, si = (int)threadIdx.x - lane * ns;
+    for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK, lane += dq, si += dr) {
+        if (si >= ns) {
+            si -= ns;
+            ++lane;
+        }
         const long cw = tile * WAVE + lane;
         const long s = s0 + si;
         if (cw >= B || s >= S) continue;

@@ -1472,13 +1472,20 @@ constexpr int DM_TAB = 512 + 64;   // LDS table: 2*M point coordinates (+ 2 * 2^
 
 // One LLR from the two per-half minima (:219-225): NaN propagates, then the
 // division by the noise variance, the +-30 clip and the caller's sign.
-template <typename T> __device__ __forceinline__ double llr_of(T lo, T hi, const DemapCfg &c) {
-    const T diff = lo - hi;
-    double v;
-    if (sizeof(T) == 4 && c.div_f32) v = (double)((float)diff / (float)c.nv);
-    else v = (double)diff / c.nv;
-    if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);   // np.clip(llr, -30, 30)
+template <typename T> __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
+    if (sizeof(T) == 4 && c.div_f32) {
+        // the f32 quotient clipped and negated in f32: the same values as in f64
+        // (f32 -> f64 is exact and so are the +-30 clip and the negation)
+        float q = (float)diff / (float)c.nv;
+        if (q == q) q = q < -30.0f ? -30.0f : (q > 30.0f ? 30.0f : q);   // np.clip(llr, -30, 30)
+        return (double)(c.sign < 0 ? -q : q);
+    }
+    double v = (double)diff / c.nv;
+    if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);
     return c.sign < 0 ? -v : v;
+}
+template <typename T> __device__ __forceinline__ double llr_of(T lo, T hi, const DemapCfg &c) {
+    return llr_from_diff<T>(lo - hi, c);
 }
 
 // Square QAM whose label splits into K I-bits and K Q-bits (16/64/256QAM of
@@ -1591,10 +1598,8 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
             const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
             const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
             const T a = cabs_fin<T>(sr - lev_i[ia], si - lev_q[iq]);
-            T m[2];
-            m[vn] = dn;
-            m[vo] = a * a;
-            out[ax * K + b] = llr_of<T>(m[0], m[1], c);
+            const T ao = a * a;
+            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
         }
     return true;
 }

@@ -1711,7 +1711,7 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
     // The half holding the overall nearest point has that point as its
     // candidate (same first-minimum rule per axis), so its distance is shared
     // by every bit: BPS + 1 numpy distances instead of 2 * BPS.
-    const T an = cabs_np<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
+    const T an = cabs_fin<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
     const T dn = an * an;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax)
@@ -1719,11 +1719,9 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
         for (int b = 0; b < K; ++b) {
             const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
             const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
-            const T a = cabs_np<T>(sr - lev_i[ia], si - lev_q[iq]);
-            T m[2];
-            m[vn] = dn;
-            m[vo] = a * a;
-            out[ax * K + b] = llr_of<T>(m[0], m[1], c);
+            const T a = cabs_fin<T>(sr - lev_i[ia], si - lev_q[iq]);
+            const T ao = a * a;
+            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
         }
     return true;
 }

@@ -166,6 +166,13 @@ int tdec_info_bits_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, uint8_t *d_
 int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const int32_t *d_bits, int32_t *d_errs,
                           void *stream);
 
+/* ---- self-test of the demapper's exact shortcuts (test infrastructure; no
+ * reference counterpart): which 0 compares the kernels' [1, 2] square root with
+ * sqrtf and the correctly rounded one for every f32 in [1, 2] (n ignored);
+ * which 1 / 2 compare the finite-input |z| with numpy's |z| (npm::cabs_np,
+ * f32 / f64) on n pseudo-random finite pairs.  *mismatches = differing results. */
+int tdec_selftest(int device, int which, long long n, unsigned long long seed, long long *mismatches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -832,6 +832,28 @@ int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void
     return rc;
 }
 
+int tdec_selftest(int device, int which, long long n, unsigned long long seed, long long *mismatches) {
+    if (!mismatches || which < 0 || which > 2 || n < 0) return fail(TDEC_EINVAL, "bad selftest arguments");
+    if (which == 0) n = (1LL << 23) + 1;   // every f32 in [1, 2]
+    *mismatches = 0;
+    if (n == 0) return 0;
+    Guard g(device);
+    unsigned long long *d = nullptr;
+    HIPCHK(hipMalloc(&d, 2 * sizeof(*d)));
+    int rc = 0;
+    if (hipMemset(d, 0, 2 * sizeof(*d)) != hipSuccess) rc = fail(TDEC_EHIP, "memset");
+    if (!rc) {
+        hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0, which, n, seed, d);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = fail(TDEC_EHIP, "selftest failed");
+    }
+    unsigned long long h[2] = {0, 0};
+    if (!rc && hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) rc = fail(TDEC_EHIP, "memcpy");
+    hipFree(d);
+    if (!rc && h[1] != (unsigned long long)n) rc = fail(TDEC_EHIP, "selftest evaluated fewer items than asked");
+    *mismatches = (long long)h[0];
+    return rc;
+}
+
 int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const void *cons, int cons_f64, int M,
                           int bps, double noise_var, int div_f32, float *d_planes, void *stream) {
     if (!h || B < 0 || !cons) return fail(TDEC_EINVAL, "bad demap arguments");

@@ -1755,6 +1755,45 @@ __global__ __launch_bounds__(BLOCK) void k_demap(const S *syms, long n_sym, cons
     for (int b = 0; b < BPS; ++b) llr[s * BPS + b] = v[b];
 }
 
+// ---- self-tests of the demapper's exact shortcuts (tdec_selftest) -------------------
+// which 0: sqrt_1_2 against sqrtf and against the correctly rounded f64 square
+// root rounded to f32 (innocuous double rounding for sqrt) for every f32 in
+// [1, 2]; which 1 / 2: cabs_fin against npm::cabs_np (f32 / f64) on n
+// splitmix64 bit patterns taken as finite (re, im) pairs, every exponent.
+// bad[0] counts differing results, bad[1] the items evaluated.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsigned long long seed,
+                                                    unsigned long long *bad) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    bool ok = true;
+    if (which == 0) {
+        const float x = __uint_as_float(0x3F800000u + (unsigned)i);
+        const unsigned a = __float_as_uint(sqrt_1_2<float>(x));
+        ok = a == __float_as_uint(sqrtf(x)) && a == __float_as_uint((float)sqrt((double)x));
+    } else if (which == 1) {
+        const unsigned long long r = splitmix64(seed + 2 * (unsigned long long)i);
+        float re = __uint_as_float((unsigned)r), im = __uint_as_float((unsigned)(r >> 32));
+        if (!isfinite(re)) re = 1.5f;
+        if (!isfinite(im)) im = -0.75f;
+        ok = __float_as_uint(cabs_fin<float>(re, im)) == __float_as_uint(cabs_np<float>(re, im));
+    } else {
+        double re = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i));
+        double im = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i + 1));
+        if (!isfinite(re)) re = 1.5;
+        if (!isfinite(im)) im = -0.75;
+        ok = __double_as_longlong(cabs_fin<double>(re, im)) == __double_as_longlong(cabs_np<double>(re, im));
+    }
+    if (!ok) atomicAdd(bad, 1ull);
+    const unsigned long long act = __ballot(1);   // bad[1]: items evaluated (a launch that did not run fails)
+    if ((threadIdx.x & (WAVE - 1)) == (unsigned)__ffsll((long long)act) - 1) atomicAdd(bad + 1, (unsigned long long)__popcll(act));
+}
+
 // Fused demap -> f32 -> de-puncture planes (the bench path).
 // One block = one 64-codeword tile x DM_KC trellis steps.  Phase 1: the
 // block's threads demap every symbol covering the LLR range of those steps

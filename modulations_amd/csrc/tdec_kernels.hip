@@ -1811,8 +1811,8 @@ constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free colu
 
 template <typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
-                                                       DemapCfg c, const int *src, const int *off, long n_avail,
-                                                       float *planes) {
+                                                       DemapCfg c, const int *__restrict__ src,
+                                                       const int *__restrict__ off, long n_avail, float *planes) {
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
     load_table<T, BPS>(cons, cons_g, c);
@@ -1849,7 +1849,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
     float *base = planes + tile * tile_floats(N);
     for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
         const int lane = t & (WAVE - 1);
-        const int q = t >> 6;                                    // (step, half)
+        const int q = __builtin_amdgcn_readfirstlane(t >> 6);   // (step, half): wave-uniform, so src[] is read by scalar loads
         const int k = k0 + q / 2, half = q & 1;
         const long cw = tile * WAVE + lane;
         const int nc = half ? 2 : 4;

@@ -1435,14 +1435,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_W
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.
 // src[c*N + k] = LLR index or -1 for the components c = X.xyzw, (unused, unused), Z.xy.
-__global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float *llr, long stride, const int *src,
-                                                     float *planes, long total) {
+__global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float *llr, long stride,
+                                                     const int *__restrict__ src, float *planes, long total) {
     const long t = (long)blockIdx.x * BLOCK + threadIdx.x;
     if (t >= total) return;                 // total = tiles * N * 64
     const int lane = (int)(t & (WAVE - 1));
-    const long q = t >> 6;                  // (tile, k)
-    const int k = (int)(q % N);
-    const long tile = q / N;
+    const long q = t >> 6;                  // (tile, k): wave-uniform, so src[] is read by scalar loads
+    const int k = __builtin_amdgcn_readfirstlane((int)(q % N));
+    const long tile = __builtin_amdgcn_readfirstlane((int)(q / N));
     const long cw = tile * WAVE + lane;
     float v[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (cw < B) {

@@ -1313,17 +1313,30 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             uint32_t w0 = 0, w1 = 0;
             double *lo = (p.lfinal && cw < p.B) ? p.lfinal + cw * nb : nullptr;
             const int kn = min(32, N - kc);
-            for (int kk = 0; kk < kn; ++kk) {
-                const int k = kc + kk;
-                const float4 x = at(X, k * WAVE + lane);
-                const double2 la = at(Le2, wsrow(inv[k], rs) + lane);
-                const double2 le = at(Le1, wsrow(k, rs) + lane);
-                const double fa = ((double)x.x + la.x) + le.x;
-                const double fb = ((double)x.y + la.y) + le.y;
-                const uint32_t two = (fa < 0.0 ? 1u : 0u) | (fb < 0.0 ? 2u : 0u);
-                if (kk < 16) w0 |= two << (2 * kk);
-                else w1 |= two << (2 * (kk - 16));
-                if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
+            // groups of 8 steps whose 24 loads are issued together (one exposed
+            // memory latency per group, not per step; 3.2 % of the decode before)
+            for (int kg = 0; kg < kn; kg += 8) {
+                float2 xa[8];
+                double2 la[8], le[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = min(kc + kg + u, N - 1);   // past the chunk: a valid row, unused
+                    const float4 x = at(X, k * WAVE + lane);
+                    xa[u] = make_float2(x.x, x.y);
+                    la[u] = at(Le2, wsrow(inv[k], rs) + lane);
+                    le[u] = at(Le1, wsrow(k, rs) + lane);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int kk = kg + u, k = kc + kk;
+                    if (kk >= kn) break;   // wave-uniform
+                    const double fa = ((double)xa[u].x + la[u].x) + le[u].x;
+                    const double fb = ((double)xa[u].y + la[u].y) + le[u].y;
+                    const uint32_t two = (fa < 0.0 ? 1u : 0u) | (fb < 0.0 ? 2u : 0u);
+                    if (kk < 16) w0 |= two << (2 * kk);
+                    else w1 |= two << (2 * (kk - 16));
+                    if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
+                }
             }
             hb[lane] = w0;
             hb[WAVE + lane] = w1;

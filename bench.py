@@ -114,8 +114,13 @@ def measured_traffic(workload, kernel):
     ent = json.load(open(tf)).get(kernel, {}).get(workload)
     if not ent:
         return None, "workload not profiled"
-    if ent.get("lib_sha256") != lib_sha256():
-        return None, "profiles/traffic.json was measured on another libtdec.so build"
+    from modulations_amd import _native
+    from modulations_amd.build import build_info
+    info = build_info(_native.LIB_PATH) or {}
+    same_lib = ent.get("lib_sha256") == lib_sha256()
+    same_src = ent.get("src_sha256") is not None and ent.get("src_sha256") == info.get("src_sha256")
+    if not (same_lib or same_src):
+        return None, "profiles/traffic.json was measured on another libtdec.so build (sources or binary)"
     return ent, None
 
 

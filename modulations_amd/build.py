@@ -7,6 +7,8 @@ hipcc cross-compiles for gfx950 without a GPU.  Flags that the numerics need:
   -ffp-contract=off                  no FMA contraction (the reference has none)
   -fno-gpu-flush-denormals-to-zero   IEEE f32 denormals, as numpy/numba
 """
+import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -33,15 +35,49 @@ def hipcc():
     return "hipcc"
 
 
+def source_digest(deps, extra=()):
+    """sha256 over the sources, the flags and the compiler version: the identity
+    of a build.  hipcc output is not byte-reproducible (a rebuild of the same
+    sources differs in a few dozen bytes of the offload bundle), so measurements
+    (profiles/traffic.json) are keyed by this digest as well as by the .so hash."""
+    h = hashlib.sha256()
+    for d in deps:
+        h.update(os.path.basename(d).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update("\0".join([*FLAGS, *extra]).encode())
+    try:
+        v = subprocess.run([hipcc(), "--version"], capture_output=True, text=True).stdout
+    except OSError:
+        v = ""
+    h.update(v.encode())
+    return h.hexdigest()
+
+
+def build_info(out):
+    """The build record written next to a library by _build_one (None if absent)."""
+    try:
+        with open(out + ".build.json") as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def _build_one(src, deps, out, force, extra):
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+    if (not force and os.path.exists(out) and os.path.exists(out + ".build.json")
+            and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)):
         return out
     cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", out, src]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc failed building {os.path.basename(out)}")
+    with open(out, "rb") as f:
+        lib_sha = hashlib.sha256(f.read()).hexdigest()
+    with open(out + ".build.json", "w") as f:
+        json.dump({"src_sha256": source_digest(deps, extra), "lib_sha256": lib_sha,
+                   "flags": [*FLAGS, *extra]}, f, indent=1)
     return out
 
 

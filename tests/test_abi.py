@@ -61,3 +61,17 @@ def test_builtin_constellations_match_the_mapper_tables():
         got = iq[0:2 * M:2] + 1j * iq[1:2 * M:2]
         assert np.array_equal(got, want.astype(np.complex128)), name
     assert L.tdec_constellation(6, _native.ptr(np.zeros(512)), C.byref(C.c_int())) == _native.TDEC_EINVAL
+
+
+def test_build_record_identifies_the_loaded_library():
+    """lib/*.build.json (written by modulations_amd.build) names the binary and the
+    source digest that profiles/traffic.json measurements are keyed by."""
+    import hashlib
+    from modulations_amd import build as B
+    for out, deps in ((B.OUT, B.DEPS), (B.MODEM_OUT, B.MODEM_DEPS)):
+        info = B.build_info(out)
+        if info is None:
+            pytest.skip("library built without a build record")
+        with open(out, "rb") as f:
+            assert info["lib_sha256"] == hashlib.sha256(f.read()).hexdigest()
+        assert info["src_sha256"] == B.source_digest(deps)

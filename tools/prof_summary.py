@@ -100,6 +100,9 @@ def main(src, dst, batch=1 << 20, workload=None):
         import hashlib
         lib = os.path.join(ROOT, "modulations_amd", "lib", "libtdec.so")
         sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+        sys.path.insert(0, ROOT)
+        from modulations_amd.build import build_info
+        src_sha = (build_info(lib) or {}).get("src_sha256")
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         tr = json.load(open(tf)) if os.path.exists(tf) else {}
         for k in ("k_turbo_decode", "k_turbo_decode_logmap"):
@@ -112,7 +115,7 @@ def main(src, dst, batch=1 << 20, workload=None):
             ent[workload] = {"hbm_bytes_per_codeword": d["hbm_bytes_per_codeword"],
                              "hbm_read_bytes_per_codeword": d["hbm_read_bytes"] / batch,
                              "hbm_write_bytes_per_codeword": d["hbm_write_bytes"] / batch,
-                             "avg_ms": d["avg_ms"], "lib_sha256": sha, "source": dst + "_summary.json",
+                             "avg_ms": d["avg_ms"], "lib_sha256": sha, "src_sha256": src_sha, "source": dst + "_summary.json",
                              "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (KiB); "
                                        f"FETCH_SIZE x {FETCH_FACTOR} (gfx950 read calibration, "
                                        "profiles/r02_fetch_cal.txt); per launch / codewords per launch"}

@@ -392,6 +392,34 @@ void tdec_destroy(tdec_t *h) {
         }
     }
 #endif
+#if TDEC_WAVE_TIMING
+    {   // measurement build: wave finish-time spread of the last decode launch
+        static unsigned long long t[WT_MAX][2];
+        static int nt[WT_MAX];
+        hipDeviceSynchronize();
+        const int n = std::min(h->max_waves, WT_MAX);
+        if (n > 0 && hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wave_t), sizeof(t)) == hipSuccess &&
+            hipMemcpyFromSymbol(nt, HIP_SYMBOL(g_wave_tiles), sizeof(nt)) == hipSuccess) {
+            unsigned long long t0 = ~0ull, t1 = 0;
+            for (int i = 0; i < n; ++i) t0 = std::min(t0, t[i][0]), t1 = std::max(t1, t[i][1]);
+            std::vector<double> end(n);
+            double busy = 0;
+            int tmin = 1 << 30, tmax = 0;
+            for (int i = 0; i < n; ++i) {
+                end[i] = (t[i][1] - t0) * 1e-5;   // ms at 100 MHz
+                busy += (t[i][1] - t[i][0]) * 1e-5;
+                tmin = std::min(tmin, nt[i]), tmax = std::max(tmax, nt[i]);
+            }
+            std::sort(end.begin(), end.end());
+            const double span = (t1 - t0) * 1e-5;
+            fprintf(stderr,
+                    "[tdec] waves %d: span %.2f ms, wave end p0 %.2f p10 %.2f p50 %.2f p90 %.2f p100 %.2f ms, "
+                    "busy %.4f of waves x span, tiles per wave %d..%d\n",
+                    n, span, end[0], end[n / 10], end[n / 2], end[n * 9 / 10], end[n - 1], busy / (n * span), tmin,
+                    tmax);
+        }
+    }
+#endif
     hipFree(h->d_perm);
     hipFree(h->d_used);
     hipFree(h->d_inv);

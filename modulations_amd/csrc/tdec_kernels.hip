@@ -1252,6 +1252,19 @@ struct PlanesIn {
     __device__ __forceinline__ void publish() const {}
 };
 
+// TDEC_WAVE_TIMING (measurement build): per persistent wave of the last decode
+// launch, {first, last} s_memrealtime (100 MHz, chip-wide) and the tiles it
+// took, printed by tdec_destroy: how much of the launch the waves spend idle
+// in the tail once the tile queue is empty.
+#ifndef TDEC_WAVE_TIMING
+#define TDEC_WAVE_TIMING 0
+#endif
+#if TDEC_WAVE_TIMING
+constexpr int WT_MAX = 16384;
+__device__ unsigned long long g_wave_t[WT_MAX][2];
+__device__ int g_wave_tiles[WT_MAX];
+#endif
+
 template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, const int *__restrict__ used,
@@ -1270,6 +1283,10 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     float4 *ring = ck + (long)nw * 4 * rs;
     double2 *sink = p.aux + WAVE + (long)wave * WAVE;
     int buf = 0;
+#if TDEC_WAVE_TIMING
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+    int wtiles = 0;
+#endif
     pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
     pro.publish();
     // Every wave starts with tile `wave`; with a tile counter the next tile is
@@ -1380,7 +1397,17 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         if (has_next) pro.publish();
         buf ^= 1;
         tile = nxt;
+#if TDEC_WAVE_TIMING
+        ++wtiles;
+#endif
     }
+#if TDEC_WAVE_TIMING
+    if (lane == 0 && wave < WT_MAX) {
+        g_wave_t[wave][0] = wt0;
+        g_wave_t[wave][1] = __builtin_amdgcn_s_memrealtime();
+        g_wave_tiles[wave] = wtiles;
+    }
+#endif
 }
 
 // Both held to 256 registers (2 waves per SIMD).  max-log: the few tile-level

@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--fused", action="store_true", help="one launch (k_turbo_decode_syms, demap inside the "
                     "decoder waves) instead of k_demap_planes + k_turbo_decode (A/B; measured slower)")
+    ap.add_argument("--overlap", action=argparse.BooleanOptionalAction, default=False,
+                    help="demap of batch i+1 on its own handle / stream / plane buffer, free to fill the tail of "
+                    "batch i's decode (DevicePipeline(overlap=True))")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
                     "several ranks on one GPU together with --all-on-device0")
     ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
@@ -198,8 +201,10 @@ def main():
     cw0 = rank * B                                   # this rank's global codewords: [rank*B, (rank+1)*B)
     t0 = time.time()
     # decoder workspace and planes first, into unfragmented HBM (placement)
-    pipe = DevicePipeline(codec, args.mod, B, device, fused=args.fused)
+    pipe = DevicePipeline(codec, args.mod, B, device, fused=args.fused, overlap=args.overlap)
     _, syms, n0 = make_symbols(codec, B, args.mod, args.ebn0, SEED, device, cw0=cw0, want_info=False)
+    syms_ready = torch.cuda.Event()
+    syms_ready.record()
     S = syms.shape[1]
     nv = np.float64(n0)
     f64, div32, nve = D.demap_mode(np.complex64, cons.dtype, nv)
@@ -210,7 +215,7 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
-        pipe.run(syms, nv, stream=stream, events=ev)
+        pipe.run(syms, nv, stream=stream, events=ev, syms_ready=syms_ready)
 
     for i in range(args.warmup):
         step()

@@ -81,12 +81,13 @@ class DevicePipeline:
     needs every wave streaming to keep HBM busy.  Buffers are sized once; run()
     is stream-ordered and allocation free."""
 
-    def __init__(self, codec, mod, B, device, fused=False):
+    def __init__(self, codec, mod, B, device, fused=False, overlap=False):
         import torch
         self.codec, self.mod, self.B = codec, mod, B
         self.bps = D.MODULATIONS[mod]["bps"]
         self.cons = D.constellation(mod)
         self.fused = bool(fused) and codec.fused_available(self.cons, self.bps)
+        self.overlap = bool(overlap) and not self.fused
         if self.fused:
             codec.reserve_fused(B)
             self.planes = None
@@ -94,10 +95,56 @@ class DevicePipeline:
             codec.reserve(B)
             self.planes = torch.empty(codec.planes_bytes(B) // 4, dtype=torch.float32, device=device)
         self.bits = torch.empty((B, codec.k_info), dtype=torch.int32, device=device)
+        if self.overlap:
+            # Batch i+1's demap runs on its own handle (handles order only their own
+            # buffers), its own low-priority stream and the other plane buffer, so
+            # it can start as soon as batch i's persistent decoder waves begin to
+            # retire (tail of the persistent launch) instead of after
+            # the last one.  The decode runs on a high-priority stream, so a decode
+            # and a demap that become ready together dispatch the decode first.
+            import copy
+            self.demapper = copy.copy(codec)
+            self.demapper._h = None
+            self.planes_db = [self.planes, torch.empty_like(self.planes)]
+            self.s_demap = torch.cuda.Stream(device=device, priority=0)
+            self.s_decode = torch.cuda.Stream(device=device, priority=-1)
+            self.demap_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.decode_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.step = 0
 
-    def run(self, syms, noise_var, stream=None, events=None):
+    def run(self, syms, noise_var, stream=None, events=None, syms_ready=None):
+        """One batch: demap -> decode, stream-ordered on `stream` (its bits are ready
+        for work queued on `stream` afterwards).  With overlap=True, `syms_ready`
+        (an event after which `syms` is valid) lets the demap start before the
+        previous batch's decode has finished; without it the demap waits for
+        everything queued on `stream`, i.e. no overlap."""
         _, div32, nve = D.demap_mode(np.complex64, self.cons.dtype, np.float64(noise_var))
         bits = self.bits[:syms.shape[0]]          # the first rows: a contiguous view
+        if self.overlap:
+            import torch
+            stream = torch.cuda.current_stream() if stream is None else stream
+            b = self.step & 1
+            sd, sk = self.s_demap, self.s_decode
+            if self.step >= 2:
+                sd.wait_event(self.decode_done[b])      # planes[b]'s last reader (batch i-2)
+            if syms_ready is not None:
+                sd.wait_event(syms_ready)
+            else:
+                sd.wait_stream(stream)
+            self.demapper.demap_planes_device(syms, self.cons, self.bps, nve, self.planes_db[b], div_f32=div32,
+                                              stream=sd)
+            self.demap_done[b].record(sd)
+            sk.wait_stream(stream)                      # earlier readers of bits on the caller's stream
+            sk.wait_event(self.demap_done[b])
+            if events is not None:
+                events[0].record(sk)
+            self.codec.decode_planes_device(self.planes_db[b], syms.shape[0], bits, stream=sk)
+            if events is not None:
+                events[1].record(sk)
+            self.decode_done[b].record(sk)
+            stream.wait_event(self.decode_done[b])
+            self.step += 1
+            return bits
         if self.fused:
             if events is not None:
                 events[0].record(stream)

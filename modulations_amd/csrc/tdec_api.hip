@@ -417,6 +417,28 @@ void tdec_destroy(tdec_t *h) {
                     "busy %.4f of waves x span, tiles per wave %d..%d\n",
                     n, span, end[0], end[n / 10], end[n / 2], end[n * 9 / 10], end[n - 1], busy / (n * span), tmin,
                     tmax);
+            // mean tiles per wave by XCD (blocks are dispatched round-robin over the 8 XCDs), by
+            // wave within the block and by the block's slot on its CU (block / 8 even or odd)
+            double x[8] = {}, wb[4] = {}, sl[2] = {};
+            int nx[8] = {}, nwb[4] = {}, nsl[2] = {};
+            for (int i = 0; i < n; ++i) {
+                const int blk = i / 4;
+                x[blk % 8] += nt[i], ++nx[blk % 8];
+                wb[i % 4] += nt[i], ++nwb[i % 4];
+                sl[(blk / 8) & 1] += nt[i], ++nsl[(blk / 8) & 1];
+            }
+            fprintf(stderr, "[tdec] tiles/wave by XCD:");
+            for (int i = 0; i < 8; ++i) fprintf(stderr, " %.2f", nx[i] ? x[i] / nx[i] : 0.0);
+            fprintf(stderr, "  by wave in block:");
+            for (int i = 0; i < 4; ++i) fprintf(stderr, " %.2f", nwb[i] ? wb[i] / nwb[i] : 0.0);
+            fprintf(stderr, "  by block/8 parity: %.2f %.2f\n", nsl[0] ? sl[0] / nsl[0] : 0.0,
+                    nsl[1] ? sl[1] / nsl[1] : 0.0);
+            int hist[16] = {};
+            for (int i = 0; i < n; ++i) ++hist[std::min(nt[i], 15)];
+            fprintf(stderr, "[tdec] tiles/wave histogram:");
+            for (int i = 0; i < 16; ++i)
+                if (hist[i]) fprintf(stderr, " %d:%d", i, hist[i]);
+            fprintf(stderr, "\n");
         }
     }
 #endif

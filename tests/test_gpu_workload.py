@@ -140,3 +140,26 @@ def test_ber_point_independent_of_world_size(tmp_path):
     for k in ("codewords", "bit_errors", "frame_errors"):
         assert one[k] == two[k], k
     assert one["codewords"] == 5000 and one["bit_errors"] > 0
+
+
+def test_overlapped_pipeline_gives_the_serial_bits():
+    """DevicePipeline(overlap=True) (next batch's demap on its own handle, stream and
+    plane buffer) decodes every batch to the serial pipeline's bits, batch after
+    batch with alternating plane buffers and different symbols per batch."""
+    from modulations_amd.workload import DevicePipeline
+    c = M.DVBRCS2_Turbo(212, "1/3")
+    B = 4096
+    serial = DevicePipeline(c, "16QAM", B, torch.device("cuda", 0))
+    c2 = M.DVBRCS2_Turbo(212, "1/3")
+    ovl = DevicePipeline(c2, "16QAM", B, torch.device("cuda", 0), overlap=True)
+    batches = [make_symbols(c, B, "16QAM", 2.0, 1234, "cuda", cw0=j * B, want_info=False) for j in range(3)]
+    ready = torch.cuda.Event()
+    ready.record()
+    want, got = [], []
+    for _, syms, n0 in batches:
+        want.append(serial.run(syms, n0).clone())
+    for _, syms, n0 in batches:
+        got.append(ovl.run(syms, n0, syms_ready=ready).clone())   # clone on the caller's stream: after the decode
+    torch.cuda.synchronize()
+    for w, g in zip(want, got):
+        assert torch.equal(w, g)

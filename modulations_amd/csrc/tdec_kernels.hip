@@ -161,6 +161,30 @@ template <int ALGO> __device__ __forceinline__ float acc_first(float t) {
     }
 }
 
+// The first max* of all 16 states at once: when every lane's smallest first
+// candidate is >= NEG + 256, |NEG - t| >= 150 holds for every state (f32
+// subtraction is monotone), so each acc_first takes its fast path; the one
+// wave-uniform test replaces 16 (a NaN candidate is dropped by the minimum and
+// gives NEG on both paths; anything else falls back to the per-state test).
+// TDEC_LM_FIRST16=0 restores the per-state tests.
+#ifndef TDEC_LM_FIRST16
+#define TDEC_LM_FIRST16 1
+#endif
+template <int ALGO> __device__ __forceinline__ void acc_first16(const float (&t)[NS], float (&m)[NS]) {
+    if constexpr (ALGO != 0 && TDEC_LM_FIRST16) {
+        float lo = t[0];
+#pragma unroll
+        for (int s = 1; s < NS; ++s) lo = fminf(lo, t[s]);
+        if (__all(lo >= NEG + 256.0f)) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) m[s] = fmaxf(NEG, t[s]) + 0.0f;
+            return;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) m[s] = acc_first<ALGO>(t[s]);
+}
+
 template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   // max_star, :32-35
     if constexpr (ALGO == 0) return a > b ? a : b;
     else return jac(a, b);
@@ -237,12 +261,17 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
     // then max* over the two predecessors in table order (p0, p0 + 8)
     float pm[2][4];
     pair_jac(g, pm);
-    float na[NS];
+    float na[NS], t0[NS];
 #pragma unroll
     for (int ns = 0; ns < NS; ++ns) {
-        const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
-        const float m = acc_first<ALGO>(a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)));
-        na[ns] = acc<ALGO>(m, a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
+        const int p0 = t_prev_s(ns, 0);
+        t0[ns] = a[p0] + pm_of(pm, p0, t_prev_i(ns, 0));
+    }
+    acc_first16<ALGO>(t0, na);
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) {
+        const int p1 = t_prev_s(ns, 2);
+        na[ns] = acc<ALGO>(na[ns], a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
     }
     const float norm = na[0];
 #pragma unroll
@@ -273,12 +302,12 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     // log-MAP: pair class {0, 3} (successor next(s, 0)) first, then {1, 2}
     float pm[2][4];
     pair_jac(g, pm);
-    float nb[NS];
+    float nb[NS], t0[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        const float m = acc_first<ALGO>(b[t_next(s, 0)] + pm_of(pm, s, 0));
-        nb[s] = acc<ALGO>(m, b[t_next(s, 1)] + pm_of(pm, s, 1));
-    }
+    for (int s = 0; s < NS; ++s) t0[s] = b[t_next(s, 0)] + pm_of(pm, s, 0);
+    acc_first16<ALGO>(t0, nb);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) nb[s] = acc<ALGO>(nb[s], b[t_next(s, 1)] + pm_of(pm, s, 1));
     const float norm = nb[0];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;

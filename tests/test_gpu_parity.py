@@ -88,6 +88,40 @@ def test_siso_extreme_inputs():
         assert np.array_equal(LeA, rA) and np.array_equal(LeB, rB)
 
 
+def test_logmap_extreme_inputs_take_both_first_maxstar_paths():
+    """log-MAP recursions test all 16 first max* of a step at once (kernel
+    acc_first16) and fall back to the per-state test when a candidate lies
+    within 256 of the -1e9 floor.  Rows of one wave mix ordinary metrics with
+    metrics at the floor (inputs of 1e9 scale), so both paths and the per-lane
+    fallback run; SISO and full decode equal the oracle bit for bit."""
+    t, _ = O.trellis()
+    n, B = 48, 9
+    rng = np.random.default_rng(5)
+    Lc = (rng.standard_normal((4, B, n)) * 4).astype(np.float32)
+    Lc[:, 0] = 1e12
+    Lc[:, 1] = -3e8
+    Lc[:, 2] = (np.sign(rng.standard_normal((4, n))) * 1e9).astype(np.float32)
+    Lc[:, 3, ::4] = 2e9
+    Lc[:, 4] = (rng.standard_normal((4, n)) * 5e8).astype(np.float32)
+    Lc[:, 5, ::7] = -1.5e9
+    Lc[:, 6] = np.float32(1e-40)
+    La = rng.standard_normal((2, B, n)) * 10
+    La[:, 7] = 3e8
+    LeA, LeB = M.bcjr_max_log_map_batch(*Lc, *La, *_tabs(), n, 0.7, algo="log-map")
+    for b in range(B):
+        rA, rB = O.siso(*Lc[:, b], *La[:, b], t, 0.7, algo=1)
+        assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b
+    c = M.DVBRCS2_Turbo(n, "1/3", algo="log-map")
+    llr = (rng.standard_normal((B, c.n_coded)) * 3).astype(np.float32)
+    llr[0] = 1e9
+    llr[1, ::3] = -2e9
+    llr[2] = (np.sign(rng.standard_normal(c.n_coded)) * 7e8).astype(np.float32)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    rb, rl = O.decode_batch(llr, n, c.punct["period"], T.puncture_matrix(c.punct), 8, c.perm, c.inv_perm, t,
+                            algo=1, want_lfinal=True)
+    assert np.array_equal(bits, rb) and np.array_equal(lf, rl)
+
+
 # ---------------------------------------------------------------- decode -----------
 def test_decode_golden(G_decode):
     keys = sorted(k[4:] for k in G_decode.files if k.startswith("llr_"))

@@ -63,7 +63,14 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse "
                     "several ranks on one GPU together with --all-on-device0")
     ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
-    return ap.parse_args()
+    ap.add_argument("--rank-deadline", type=float, default=1800.0,
+                    help="--gpus N without torchrun: kill every rank and exit non-zero after this many seconds")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="torch.distributed timeout (s) for rendezvous and collectives")
+    a = ap.parse_args()
+    if a.all_on_device0 and a.gpus > 1 and a.dist_backend == "nccl":
+        ap.error("--all-on-device0 puts several ranks on one GPU, which RCCL cannot do: add --dist-backend gloo")
+    return a
 
 
 def _free_port():
@@ -74,15 +81,24 @@ def _free_port():
     return p
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, argv=None, deadline=None, script=None, poll=0.2):
     """`python bench.py --gpus N`: start N rank processes (one per GPU) and wait.
-    Nothing in this parent initialises HIP; the children are fresh processes."""
+
+    Nothing in this parent initialises HIP; the children are fresh processes
+    (never an exec of a process that touched the GPU).  Fail fast: when one rank
+    exits non-zero the others are killed at once (they would wait at a barrier
+    forever), and past `deadline` seconds every rank still running is killed and
+    the return code is non-zero (124, as timeout(1)).  Returns the first
+    non-zero exit code, or 0."""
     port = _free_port()
+    argv = sys.argv[1:] if argv is None else argv
+    script = os.path.abspath(__file__) if script is None else script
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env))
+    t_end = None if deadline is None else time.monotonic() + deadline
     rc = 0
     try:
         while procs:
@@ -91,11 +107,20 @@ def spawn_ranks(n):
                 if c is None:
                     continue
                 procs.remove(p)
-                if c != 0:
-                    rc = rc or c
-                    for q in procs:        # one rank failed: the others would wait at a barrier forever
+                if c != 0 and not rc:
+                    rc = c
+                    log(f"[spawn] a rank exited with {c}: stopping the other {len(procs)}")
+                    for q in procs:
                         q.kill()
-            time.sleep(0.2)
+            if procs and t_end is not None and time.monotonic() > t_end:
+                log(f"[spawn] deadline of {deadline:.0f}s passed with {len(procs)} rank(s) running: killing them")
+                for q in procs:
+                    q.kill()
+                rc = rc or 124
+                for q in procs:
+                    q.wait()
+                procs = []
+            time.sleep(poll)
     finally:
         for p in procs:
             p.kill()
@@ -171,7 +196,7 @@ def cpu_baseline(codec, syms_host, cons, bps, nv, div32, seconds):
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, deadline=args.rank_deadline))
 
     import torch
     from modulations_amd import demap as D
@@ -187,11 +212,13 @@ def main():
     dev_idx = 0 if args.all_on_device0 else local
     torch.cuda.set_device(dev_idx)
     if dist:
+        import datetime
         import torch.distributed as tdist
+        to = datetime.timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx), timeout=to)
         else:
-            tdist.init_process_group(args.dist_backend)
+            tdist.init_process_group(args.dist_backend, timeout=to)
     device = torch.device("cuda", dev_idx)
 
     codec = M.DVBRCS2_Turbo(args.n, args.rate, 8, algo=args.algo, device=device.index)

@@ -153,8 +153,8 @@ long tdec_encoded_len(const tdec_t *h);
  * Needs n_couples % 4 == 0 and n_couples <= 1024 (every DVB-RCS2 block size). */
 
 /* info bits -> encode (as tdec_encode_dev) -> label-ordered constellation
- * (cons_iq: M host (re, im) float pairs, label = bps coded bits MSB first, the
- * last symbol zero-padded) -> complex AWGN of std-dev sigma per dimension
+ * (cons_iq: M = 2^bps host (re, im) float pairs, label = bps coded bits MSB
+ * first, the last symbol zero-padded; any other M is TDEC_EINVAL) -> complex AWGN of std-dev sigma per dimension
  * (Box-Muller on philox4x32_10({g_lo, g_hi, s/2, 0x2B0E}, seed)).  d_syms:
  * complex64 [B][ceil(n_out / bps)]; d_info (nullable): uint8 [B][2N]. */
 int tdec_workload_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const float *cons_iq, int M, int bps,

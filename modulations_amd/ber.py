@@ -10,8 +10,14 @@ Each rank owns a contiguous range of global codeword indices per point
 counter-based generator (seed per point, counter = global codeword index: the
 data, and so the counters, are the same for any world size or batch size),
 runs the fused demap + decode, and counts bit / frame errors on the device;
-only those int64 counters are all-reduced.  Finished points are written to --out after every point, and a
-rerun skips them (checkpoint / resume).
+only those int64 counters are all-reduced.  Finished points are written to
+--out after every point, and a rerun skips them (checkpoint / resume, SURVEY
+§5).  The file records the sweep's configuration and the generator version;
+a rerun into it with any other configuration (modulation, block size, rate,
+algorithm, iterations, interleaver, codewords per point, base seed) or
+generator is refused instead of mixing two data streams, and each point's
+generator key is derived from its Eb/N0 value (not its index in --ebn0), so a
+resumed sweep over a different grid regenerates exactly the same data.
 """
 from __future__ import annotations
 
@@ -21,6 +27,48 @@ import os
 import time
 
 import numpy as np
+
+
+GENERATOR = "philox4x32-10/global-codeword-index/v2"   # workload.make_symbols' stream; bump on any change
+
+
+def ebn0_seed(base_seed, ebn0_db):
+    """Generator key of the point at `ebn0_db`: the base seed and the Eb/N0
+    value in milli-dB, so the key does not depend on the point's position in
+    the sweep grid (64-bit, as the device generator takes it)."""
+    return (int(base_seed) * 1_000_003 + int(round(float(ebn0_db) * 1000)) * 7919) & 0xFFFFFFFFFFFFFFFF
+
+
+def sweep_config(a):
+    """What a results file is keyed on (argparse namespace -> dict)."""
+    return {"generator": GENERATOR, "mod": a.mod, "n_couples": int(a.n), "rate": a.rate, "algo": a.algo,
+            "iterations": int(a.iterations), "interleaver": a.interleaver, "codewords": int(a.codewords),
+            "seed": int(a.seed)}
+
+
+def load_resume(path, cfg):
+    """Finished points of `path` for the sweep configuration `cfg`:
+    {ebn0_db: record}.  A missing file is an empty sweep; a file written for
+    another configuration or generator (or in the old unkeyed list format)
+    raises ValueError rather than silently merging points of two streams."""
+    if not path or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    if not isinstance(doc, dict) or "config" not in doc:
+        raise ValueError(f"{path}: results without a sweep configuration (old format); use another --out")
+    if doc["config"] != cfg:
+        diff = {k: (doc["config"].get(k), cfg.get(k)) for k in set(doc["config"]) | set(cfg)
+                if doc["config"].get(k) != cfg.get(k)}
+        raise ValueError(f"{path}: written for another sweep configuration {diff} (file, this run); use another --out")
+    return {float(r["ebn0_db"]): r for r in doc["points"]}
+
+
+def save_results(path, cfg, results):
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump({"config": cfg, "points": sorted(results, key=lambda r: r["ebn0_db"])}, f, indent=1)
+    os.replace(tmp, path)
 
 
 def parse_points(spec):
@@ -68,45 +116,54 @@ def main(argv=None):
     ap.add_argument("--out", default=None)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on the node; gloo to rehearse")
     ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0, help="torch.distributed timeout (s)")
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.all_on_device0 and world > 1 and a.dist_backend == "nccl":
+        ap.error("--all-on-device0 puts several ranks on one GPU, which RCCL cannot do: add --dist-backend gloo")
+    cfg = sweep_config(a)
+    try:
+        done = load_resume(a.out, cfg)
+    except ValueError as e:
+        ap.error(str(e))
     dev_idx = 0 if a.all_on_device0 else local
     torch.cuda.set_device(dev_idx)
     if world > 1:
+        import datetime
+        to = datetime.timedelta(seconds=a.dist_timeout)
         if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx), timeout=to)
         else:
-            dist.init_process_group(a.dist_backend)
+            dist.init_process_group(a.dist_backend, timeout=to)
     device = torch.device("cuda", dev_idx)
     codec = M.DVBRCS2_Turbo(a.n, a.rate, a.iterations, algo=a.algo, interleaver=a.interleaver,
                             device=device.index)
     pipe = DevicePipeline(codec, a.mod, a.batch, device)
-    done = {}
-    if a.out and os.path.exists(a.out):
-        done = {float(r["ebn0_db"]): r for r in json.load(open(a.out))}
     results = list(done.values())
-    for pi, e in enumerate(parse_points(a.ebn0)):
+    for e in parse_points(a.ebn0):
         if e in done:
             continue
         start, count = S.shard_range(a.codewords, world, rank)
         t0 = time.time()
-        cnt = run_point(pipe, codec, a.mod, e, start, count, a.batch, S.point_seed(a.seed, pi), device)
+        cnt = run_point(pipe, codec, a.mod, e, start, count, a.batch, ebn0_seed(a.seed, e), device)
         if world > 1 and a.dist_backend != "nccl":
             cnt = cnt.cpu()
         S.reduce_counters(cnt, dist if world > 1 else None)
         torch.cuda.synchronize()
         be, fe, ncw = (int(x) for x in cnt.tolist())
-        rec = {"ebn0_db": e, "mod": a.mod, "n_couples": a.n, "rate": a.rate, "algo": a.algo, "codewords": ncw,
+        dt = time.time() - t0
+        rec = {"ebn0_db": e, "mod": a.mod, "n_couples": a.n, "rate": a.rate, "algo": a.algo,
+               "interleaver": a.interleaver, "codewords": ncw,
                "bit_errors": be, "frame_errors": fe, "ber": be / (ncw * codec.k_info), "fer": fe / ncw,
-               "seconds": time.time() - t0, "gpus": world}
+               "seconds": dt, "codewords_per_s": ncw / dt, "gpus": world}
         results.append(rec)
         if rank == 0:
             print(json.dumps(rec), flush=True)
             if a.out:
-                json.dump(sorted(results, key=lambda r: r["ebn0_db"]), open(a.out, "w"), indent=1)
+                save_results(a.out, cfg, results)
     if world > 1:
         dist.destroy_process_group()
     return results

@@ -362,7 +362,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
-    const long row_units = std::max<long>(rows_of(N), 4L * ((N + WIN_MIN - 1) / WIN_MIN + RING));
+    const long row_units = std::max<long>(rows_of(N), 4L * ((N + ck_win_of(algo) - 1) / ck_win_of(algo) + RING));
     const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
     h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
     // experiment knob: run the persistent decoder on a percentage of the resident waves
@@ -476,7 +476,8 @@ static int n_tiles_of(int B) { return (B + WAVE - 1) / WAVE; }
 
 // Per-wave workspace strides (elements).
 static long ws_stride_of(const tdec_t *h) { return 3L * rows_of(h->N) * WAVE; }
-static long ck_stride_of(const tdec_t *h) { return (long)((h->N + WIN_MIN - 1) / WIN_MIN + RING) * 4 * WAVE; }
+static int ck_rows_of(const tdec_t *h) { return (h->N + ck_win_of(h->algo) - 1) / ck_win_of(h->algo); }
+static long ck_stride_of(const tdec_t *h) { return (long)(ck_rows_of(h) + RING) * 4 * WAVE; }
 
 // The decoders' tile queue: the counter zeroed on the launch's stream, or null
 // (static striding) below 4 tiles per wave or with TDEC_DYN_TILES=0.  Measured
@@ -503,7 +504,7 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size
                              hipEvent_t e0, hipEvent_t e1) {
     const int B = waves * WAVE;
     DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used,
-                 h->row_pad, (double2 *)(ws + aux_off)};
+                 h->row_pad, (double2 *)(ws + aux_off), nullptr, ck_rows_of(h)};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
     float best = 1e30f;
@@ -665,7 +666,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
-                 h->aux_p, tile_queue(h, tiles, waves, st)};
+                 h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, st,
@@ -726,8 +727,9 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     if (rc) return rc;
     if (nbuf == 2 && !h->cstream) HIPCHK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
     hipStream_t cs = nbuf == 2 ? h->cstream : h->stream;
-    DrainOnExit drain{h->stream, cs};   // declared before the events: they die after the drain
     EventPair up, dec;
+    // declared after the events, so it is destroyed (drains the streams) before they are
+    DrainOnExit drain{h->stream, cs};
     if ((rc = up.create()) || (rc = dec.create())) return rc;
     float *dl = (float *)h->h_llr.p;
     int32_t *db = (int32_t *)h->h_bits.p;
@@ -961,8 +963,9 @@ int tdec_workload_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const float 
                       double sigma, float *d_syms, uint8_t *d_info, void *stream) {
     if (!h || B < 0 || cw0 < 0) return fail(TDEC_EINVAL, "bad workload arguments");
     if (B == 0) return 0;
-    if (!cons_iq || !d_syms || bps < 1 || bps > 8 || M < 1 || M > (1 << bps) || !(sigma >= 0.0))
-        return fail(TDEC_EINVAL, "bad workload arguments");
+    // every bps-bit label indexes the table, so it must hold all 2^bps points
+    if (!cons_iq || !d_syms || bps < 1 || bps > 8 || M != (1 << bps) || !(sigma >= 0.0))
+        return fail(TDEC_EINVAL, "bad workload arguments (the constellation must have 2^bps points)");
     if (!staged_encoder_ok(h)) return fail(TDEC_EINVAL, "workload generation needs N % 4 == 0 and N <= 1024");
     Guard g(h->device);
     WorkloadArgs a = workload_args(h, B);
@@ -1056,7 +1059,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
-                 h->aux_p, tile_queue(h, tiles, waves, st)};
+                 h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};

@@ -1082,7 +1082,12 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     }
     float a0[NS];
     ck_read(st.ck, lane, a0);
-    ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);   // after the slot's last read (an earlier read returns the old bytes)
+    // The slot's last read must have returned before the DMA that overwrites it is
+    // issued: the ISA does not order an outstanding ds_read against a later LDS-DMA
+    // write, and the compiler's wait-count pass cannot see the asm DMA.  a0 is
+    // needed at once by the bottom half, so the wait costs nothing.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
     window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
@@ -1214,8 +1219,6 @@ constexpr int WIN_ML = TDEC_WIN_ML;
 #endif
 constexpr int WIN_LM = TDEC_WIN_LM;      // log-MAP turbo decoder's checkpoint interval
 __host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_ML; }
-// the workspace's checkpoint array is sized for the densest interval in use
-constexpr int WIN_MIN = WIN < WIN_ML ? (WIN < WIN_LM ? WIN : WIN_LM) : (WIN_ML < WIN_LM ? WIN_ML : WIN_LM);
 constexpr int LDS_STAGE1 = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
 constexpr int LDS_STAGE = LDS_STAGE1 * 2;   // double-buffered (siso8)
 // siso8's LDS per block: lv = 2 staging buffers + the checkpoint slots (float4),
@@ -1230,6 +1233,11 @@ constexpr int EPI_STRIDE_ML = TDEC_WIN_ML == 8 ? 4 * WAVE * 4 : 2 * WAVE;   // u
 // checkpoints every 4 (max-log, the fused demap-decode kernel) or WIN_LM.
 constexpr bool STAGED_ML = WIN_ML == 8;
 __host__ __device__ constexpr int win_unstaged(int algo) { return algo ? WIN_LM : 4; }
+// A handle's checkpoint rows are sized for the densest interval among the kernels
+// that can run for its algorithm: the row SISO (WIN), the tile decoder
+// (win_of) and the fused demap-decode kernel (win_unstaged).
+__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
+__host__ __device__ constexpr int ck_win_of(int algo) { return cmin(WIN, cmin(win_of(algo), win_unstaged(algo))); }
 template <int ALGO, bool RAG, bool STAGED, class In, class Out>
 __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs,
                                          int lane, double sf, float4 *lv, double2 *ll) {
@@ -1255,13 +1263,14 @@ struct DecodeArgs {
     int B, N, iters, n_tiles, n_waves;
     const float *planes;     // [n_tiles] x (X, Z)
     double2 *ws;             // [3][N][n_waves][64]: P1, Le2, Le1 (last iteration)
-    float4 *ck;              // [ceil(N/WIN) + RING][4][n_waves][64]: alpha checkpoints, beta1 ring
+    float4 *ck;              // [ck_rows + RING][4][n_waves][64]: alpha checkpoints, beta1 ring
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
     int row_pad;             // lanes of padding after each workspace row (0 unless TDEC_ROW_PAD)
     double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
     int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
+    int ck_rows;             // checkpoint rows before the beta1 ring: ceil(N / ck_win_of(algo))
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1307,7 +1316,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
     const unsigned rs = (unsigned)p.n_waves * WAVE + (unsigned)p.row_pad;
     double2 *P1 = p.ws + (long)wave * WAVE * WS_G, *Le2 = P1 + (long)rows_of(N) * rs, *Le1 = Le2 + (long)rows_of(N) * rs;
-    const int nw = (N + WIN_MIN - 1) / WIN_MIN;
+    const int nw = p.ck_rows;
     float4 *ck = p.ck + (long)wave * WAVE * WS_G;
     float4 *ring = ck + (long)nw * 4 * rs;
     double2 *sink = p.aux + WAVE + (long)wave * WAVE;

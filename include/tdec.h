@@ -172,6 +172,15 @@ int tdec_count_errors_dev(tdec_t *h, int B, int64_t cw0, uint64_t seed, const in
  * which 1 / 2 compare the finite-input |z| with numpy's |z| (npm::cabs_np,
  * f32 / f64) on n pseudo-random finite pairs.  *mismatches = differing results. */
 int tdec_selftest(int device, int which, long long n, unsigned long long seed, long long *mismatches);
+/* which 3 (same entry point): the log-MAP primitives outside the captured
+ * tables -- every f32 t >= 48 gives 0 <= v_exp_f32(-t) <= 2^-39 (+0 at t = inf),
+ * NaN -> NaN for v_exp_f32 and v_log_f32, v_log_f32(1) = 0 (n, seed ignored).
+ *
+ * The exact outputs of the log-MAP primitives (the oracle's tables,
+ * oracle/tdec_oracle.c orc_set_trans): out[i] = v_exp_f32(-t) (which 0) or
+ * v_log_f32(w) (which 1) for the f32 whose bit pattern is lo_bits + i, i < n;
+ * out is a host buffer of n floats. */
+int tdec_selftest_trans(int device, int which, uint32_t lo_bits, long long n, float *out);
 
 #ifdef __cplusplus
 }

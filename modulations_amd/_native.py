@@ -27,7 +27,7 @@ EXPORTS = (
     "tdec_reserve", "tdec_planes_bytes", "tdec_depuncture_dev", "tdec_decode_planes_dev", "tdec_decode_batch_dev",
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
-    "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest",
+    "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
 )
 
 _lib = None
@@ -73,6 +73,7 @@ def _declare(L):
     L.tdec_demap_decode_dev.argtypes = [_vp, C.c_int, _vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                         C.c_int, _vp, _vp, _vp]
     L.tdec_selftest.argtypes = [C.c_int, C.c_int, C.c_longlong, C.c_ulonglong, C.POINTER(C.c_longlong)]
+    L.tdec_selftest_trans.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_longlong, _vp]
     for name in EXPORTS:
         f = getattr(L, name)
         if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",
@@ -81,7 +82,7 @@ def _declare(L):
                                             "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_demap_batch",
                                             "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev",
                                             "tdec_count_errors_dev", "tdec_reserve_fused", "tdec_fused_available",
-                                            "tdec_demap_decode_dev", "tdec_selftest"):
+                                            "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans"):
             f.restype = C.c_int
 
 

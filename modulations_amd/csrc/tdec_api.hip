@@ -885,8 +885,9 @@ int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void
 }
 
 int tdec_selftest(int device, int which, long long n, unsigned long long seed, long long *mismatches) {
-    if (!mismatches || which < 0 || which > 2 || n < 0) return fail(TDEC_EINVAL, "bad selftest arguments");
+    if (!mismatches || which < 0 || which > 3 || n < 0) return fail(TDEC_EINVAL, "bad selftest arguments");
     if (which == 0) n = (1LL << 23) + 1;   // every f32 in [1, 2]
+    if (which == 3) n = 0x7F800000LL - 0x42400000LL + 1;   // every f32 t in [48, +inf]
     *mismatches = 0;
     if (n == 0) return 0;
     Guard g(device);
@@ -903,6 +904,22 @@ int tdec_selftest(int device, int which, long long n, unsigned long long seed, l
     hipFree(d);
     if (!rc && h[1] != (unsigned long long)n) rc = fail(TDEC_EHIP, "selftest evaluated fewer items than asked");
     *mismatches = (long long)h[0];
+    return rc;
+}
+
+int tdec_selftest_trans(int device, int which, uint32_t lo_bits, long long n, float *out) {
+    if (!out || which < 0 || which > 1 || n < 0 || (unsigned long long)lo_bits + (unsigned long long)n > (1ull << 32))
+        return fail(TDEC_EINVAL, "bad selftest_trans arguments");
+    if (n == 0) return 0;
+    Guard g(device);
+    float *d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)n * sizeof(float)));
+    int rc = 0;
+    hipLaunchKernelGGL(k_trans_table, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, 0, which, lo_bits, n, d);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = fail(TDEC_EHIP, "selftest_trans failed");
+    if (!rc && hipMemcpy(out, d, (size_t)n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(TDEC_EHIP, "memcpy");
+    hipFree(d);
     return rc;
 }
 

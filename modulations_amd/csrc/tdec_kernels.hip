@@ -54,8 +54,14 @@ __host__ __device__ constexpr int t_prev_i(int ns, int idx) {
 // bB*4 + bW*2 + bY with bA = 0.
 // Branch metrics from the channel+a-priori sums inA = f64(Lc_A) + La_A,
 // inB likewise (:135-136), and the parities (:138-139).
+// log-MAP (ALGO 1) keeps its metrics in bits: the half weight is 0.5 * log2(e)
+// instead of 0.5 (see the log-MAP section below).
+constexpr double LM_K = 0x1.71547652b82fep-1;     // 0.5 * log2(e)
+constexpr double LM_LN2 = 0x1.62e42fefa39efp-1;   // ln 2: bits -> nats
+template <int ALGO = 0>
 __device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w, float y, float (&g)[8]) {
-    const double hA = inA * 0.5, hB = inB * 0.5, hW = (double)w * 0.5, hY = (double)y * 0.5;
+    constexpr double hw = ALGO ? LM_K : 0.5;
+    const double hA = inA * hw, hB = inB * hw, hW = (double)w * hw, hY = (double)y * hw;
     const double l1[2] = {hA + hB, hA + (-hB)};
 #pragma unroll
     for (int bB = 0; bB < 2; ++bB)
@@ -67,11 +73,12 @@ __device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w,
         }
 }
 
+template <int ALGO = 0>
 __device__ __forceinline__ void make_gamma(float a, float b, double laA, double laB, float w, float y,
                                            float (&g)[8], double &inA, double &inB) {
     inA = (double)a + laA;
     inB = (double)b + laB;
-    gamma_from_sums(inA, inB, w, y, g);
+    gamma_from_sums<ALGO>(inA, inB, w, y, g);
 }
 
 __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
@@ -79,116 +86,59 @@ __device__ __forceinline__ float gam(const float (&g)[8], int s, int inp) {
     return bA == 0 ? g[bB * 4 + bW * 2 + bY] : -g[(bB ^ 1) * 4 + (bW ^ 1) * 2 + (bY ^ 1)];
 }
 
-// ---- max / max* ---------------------------------------------------------------
-// log-MAP (build-defined): max(a,b) + log1p(exp(-|a-b|)) (the
-// historic _jacobian_log-22 cut it off at 37; here the exponential itself
-// underflows to 0 past 104).  The correction is defined as this exact sequence of f32
-// IEEE operations (explicit fused multiply-adds, no division), the same
-// sequence the oracle restates, so log-MAP is bit-exact too.  In the
-// recursions each state's two parallel branches are combined first,
-// max*(m + g, m + g') = m + max*(g, g') (exact in real arithmetic), so an alpha
-// or beta step costs 8 shared pair max* + 16, not 48; the extrinsic keeps one
-// max* per branch.  Result: within 4e-6 of log-MAP with exact f64 Jacobian
-// logarithms (tests/test_oracle_golden.py).
-__device__ __forceinline__ float exp_neg(float d) {           /* exp(-d), 0 <= d <= 150 */
-    const float x = d * 0x1.715476p+0f;                     /* d * log2(e) */
-    // n = trunc(x) and f = x - n (exact, in [0, 1)) as v_cvt_i32_f32 of -x and
-    // v_fract_f32 of x: the oracle's (int)x / x - (float)n, two instructions fewer
-    const int nn = (int)(-x);                                 /* -n */
-    const float f = __builtin_amdgcn_fractf(x);
-    float p = -0x1.f0ca8p-11f;                                /* 2^-f */
-    p = fmaf(p, f, 0x1.2dd26cp-7f);
-    p = fmaf(p, f, -0x1.c503aep-5f);
-    p = fmaf(p, f, 0x1.ebe33ap-3f);
-    p = fmaf(p, f, -0x1.62e3aap-1f);
-    p = fmaf(p, f, 0x1.fffffep-1f);
-    return ldexpf(p, nn);
-}
-__device__ __forceinline__ float log1p_01(float e) {          /* log1p(e), e in [0, 1] */
-    float q = -0x1.18f998p-7f;                                /* log1p(e) / e */
-    q = fmaf(q, e, 0x1.6a33e2p-5f);
-    q = fmaf(q, e, -0x1.b9c4c8p-4f);
-    q = fmaf(q, e, 0x1.6ba9f2p-3f);
-    q = fmaf(q, e, -0x1.f5c086p-3f);
-    q = fmaf(q, e, 0x1.54bf8p-2f);
-    q = fmaf(q, e, -0x1.fff95p-2f);
-    q = fmaf(q, e, 0x1.fffffap-1f);
-    return q * e;
-}
-__device__ __forceinline__ float jac_corr(float d) { return log1p_01(exp_neg(d)); }
-// log(S) for a positive normal S: S = 2^k (1 + u), u in [0, 1) exact, log = k ln2 + log1p(u)
-__device__ __forceinline__ float log_pos(float S) {
-    const int bits = __float_as_int(S);
-    const int k = (bits >> 23) - 127;
-    const float u = __int_as_float((bits & 0x7FFFFF) | 0x3F800000) - 1.0f;
-    return fmaf((float)k, 0x1.62e43p-1f, log1p_01(u));
-}
-// log-MAP marginal over the 16 states (the extrinsic's app[inp], build-defined):
-// M = max_s t[s] (maxNum), S = sum_s exp(-(M - t[s])) in state order with the
-// difference clamped to 150, app = M + log(S).  The log-sum-exp of 16 terms
-// costs 16 exponentials and one logarithm instead of a chain of 15 Jacobian
-// logarithms (15 of each), and is the exact f64 reference's definition
-// (np.logaddexp.reduce over the states) up to f32 rounding.
-__device__ __forceinline__ float lse16(const float (&t)[NS]) {
-    float m = t[0];
-#pragma unroll
-    for (int s = 1; s < NS; ++s) m = fmaxf(m, t[s]);
-    float S = 0.0f;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) S += exp_neg(fminf(m - t[s], 150.0f));
-    return m + log_pos(S);
-}
+// ---- log-MAP max* (build-defined; round 3) ----------------------
+// Metrics in bits (base-2 logarithms; branch metrics weighted 0.5*log2(e), the
+// extrinsic converted back to nats by one f64 multiply by ln 2), so the Jacobian
+// logarithm is maxNum(a, b) + log2(1 + 2^-|a-b|), evaluated by the hardware's
+// v_exp_f32 / v_log_f32 on a quantised argument:
+//     t = |a - b| + 8,  w = fma(v_exp_f32(-t), 256, 1),  max* = maxNum(a, b) + v_log_f32(w)
+// (7 VALU operations, two of them transcendental: 16.9 ns per wave-max* per SIMD
+// against 32.4 for round 2's exp / log1p polynomials, tools/mb/jac_rate.hip).
+// The +8 puts the instruction's argument on a bounded f32 grid (2^-20 below
+// |a-b| = 8), so its exact outputs form a finite table: the instructions are
+// faithful, not correctly rounded (tools/mb/trans_char.hip), and the oracle
+// (oracle/tdec_oracle.c, which spells out the whole definition) reproduces them
+// bit for bit from the device's exhaustive tables (tdec_selftest_trans).
+constexpr float LM_C = 8.0f, LM_SCALE = 256.0f;   // t = |a - b| + LM_C, 2^LM_C
+__device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }   // v_exp_f32
+__device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }    // v_log_f32
 
-// max*(a, b) = maxNum(a, b) + log1p(exp(-min(|a - b|, 150))): the correction is
-// exactly 0 from |a - b| > 104 on (exp underflows), a NaN operand is dropped.
 __device__ __forceinline__ float jac(float a, float b) {
-    return fmaxf(a, b) + jac_corr(fminf(fabsf(a - b), 150.0f));
+    const float t = fabsf(a - b) + LM_C;
+    const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
+    return fmaxf(a, b) + hw_log2(w);
 }
 
-template <int ALGO> __device__ __forceinline__ float acc(float m, float t) {
-    if constexpr (ALGO == 0) return fmaxf(m, t);
-    else return jac(m, t);
+// log2(2^x0 + 2^x1 + 2^x2 + 2^x3): the terms against Mc = max + 8, summed in
+// order by fma, plus Mc - 8 (exact: the maximum rounded to Mc's grid, the shift
+// the terms were taken against).
+__device__ __forceinline__ float lse4(float x0, float x1, float x2, float x3) {
+    const float Mc = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)) + LM_C;
+    float S = hw_exp2(-(Mc - x0)) * LM_SCALE;   // = fma(e, 256, 0): exact
+    S = fmaf(hw_exp2(-(Mc - x1)), LM_SCALE, S);
+    S = fmaf(hw_exp2(-(Mc - x2)), LM_SCALE, S);
+    S = fmaf(hw_exp2(-(Mc - x3)), LM_SCALE, S);
+    return (Mc - LM_C) + hw_log2(S);
 }
 
-// acc(NEG, t): the first step of every running max*.  |NEG - t| >= 150 for any
-// metric above -1e9 + 150, where the correction is exactly 0, so the wave
-// skips it unless some lane needs it (the same bits either way).
-template <int ALGO> __device__ __forceinline__ float acc_first(float t) {
-    if constexpr (ALGO == 0) return fmaxf(NEG, t);
-    else {
-        if (__all(fabsf(NEG - t) >= 150.0f)) return fmaxf(NEG, t) + 0.0f;
-        return jac(NEG, t);
-    }
-}
-
-// The first max* of all 16 states at once: when every lane's smallest first
-// candidate is >= NEG + 256, |NEG - t| >= 150 holds for every state (f32
-// subtraction is monotone), so each acc_first takes its fast path; the one
-// wave-uniform test replaces 16 (a NaN candidate is dropped by the minimum and
-// gives NEG on both paths; anything else falls back to the per-state test).
-// TDEC_LM_FIRST16=0 restores the per-state tests.
-#ifndef TDEC_LM_FIRST16
-#define TDEC_LM_FIRST16 1
-#endif
-template <int ALGO> __device__ __forceinline__ void acc_first16(const float (&t)[NS], float (&m)[NS]) {
-    if constexpr (ALGO != 0 && TDEC_LM_FIRST16) {
-        float lo = t[0];
-#pragma unroll
-        for (int s = 1; s < NS; ++s) lo = fminf(lo, t[s]);
-        if (__all(lo >= NEG + 256.0f)) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s) m[s] = fmaxf(NEG, t[s]) + 0.0f;
-            return;
+// The extrinsic's state groups: for input class c (0: inputs {0, 3}, 1: {1, 2},
+// the same A^B and so the same successor and parity bits) the 4 states, in
+// state order, whose class-c branches carry the parity pair wy = 2W + Y.
+struct LmGroups {
+    int s[2][4][4];
+};
+__host__ __device__ constexpr LmGroups make_lm_groups() {
+    LmGroups G{};
+    for (int c = 0; c < 2; ++c) {
+        int cnt[4] = {0, 0, 0, 0};
+        for (int s = 0; s < 16; ++s) {
+            const int wy = 2 * t_ow(s, c) + t_oy(s, c);
+            G.s[c][wy][cnt[wy]++] = s;
         }
     }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) m[s] = acc_first<ALGO>(t[s]);
+    return G;
 }
-
-template <int ALGO> __device__ __forceinline__ float star(float a, float b) {   // max_star, :32-35
-    if constexpr (ALGO == 0) return a > b ? a : b;
-    else return jac(a, b);
-}
+constexpr LmGroups LM_GROUPS = make_lm_groups();
 
 // ---- recursions -----------------------------------------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32: two IEEE f32 adds per lane
@@ -261,17 +211,11 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
     // then max* over the two predecessors in table order (p0, p0 + 8)
     float pm[2][4];
     pair_jac(g, pm);
-    float na[NS], t0[NS];
+    float na[NS];
 #pragma unroll
     for (int ns = 0; ns < NS; ++ns) {
-        const int p0 = t_prev_s(ns, 0);
-        t0[ns] = a[p0] + pm_of(pm, p0, t_prev_i(ns, 0));
-    }
-    acc_first16<ALGO>(t0, na);
-#pragma unroll
-    for (int ns = 0; ns < NS; ++ns) {
-        const int p1 = t_prev_s(ns, 2);
-        na[ns] = acc<ALGO>(na[ns], a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
+        const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
+        na[ns] = jac(a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)), a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
     }
     const float norm = na[0];
 #pragma unroll
@@ -302,12 +246,9 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     // log-MAP: pair class {0, 3} (successor next(s, 0)) first, then {1, 2}
     float pm[2][4];
     pair_jac(g, pm);
-    float nb[NS], t0[NS];
+    float nb[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) t0[s] = b[t_next(s, 0)] + pm_of(pm, s, 0);
-    acc_first16<ALGO>(t0, nb);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) nb[s] = acc<ALGO>(nb[s], b[t_next(s, 1)] + pm_of(pm, s, 1));
+    for (int s = 0; s < NS; ++s) nb[s] = jac(b[t_next(s, 0)] + pm_of(pm, s, 0), b[t_next(s, 1)] + pm_of(pm, s, 1));
     const float norm = nb[0];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
@@ -330,14 +271,12 @@ template <int E> __device__ __forceinline__ f2 pk_add_bcast(f2 t, f2 y) {
     return r;
 }
 
-#ifndef TDEC_LM_LSE
-#define TDEC_LM_LSE 1
-#endif
 template <int ALGO>
 __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)[8], const float (&b1)[NS], double inA,
                                           double inB, double sf, double &leA, double &leB) {
-    float app[4];
+    float LpA, LpB;
     if constexpr (ALGO == 0) {
+        float app[4];
         // (a[s] + gamma) + beta for the two inputs of a parallel pair (same next
         // state) in one lane-pair: gamma pair {g(A B wy), g(~A ~B wy)} = {g[i], -g[j]}
         // from the register pairs GP = {g0,g3}, {g1,g2}, {g4,g7}, {g5,g6}.
@@ -362,30 +301,42 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
                 app[hi] = fmaxf(app[hi], t.y);
             }
         }
+        // max_star (:32-35)
+        LpA = (app[0] > app[1] ? app[0] : app[1]) - (app[2] > app[3] ? app[2] : app[3]);
+        LpB = (app[0] > app[2] ? app[0] : app[2]) - (app[1] > app[3] ? app[1] : app[3]);
     } else {
-#if TDEC_LM_LSE
+        // log-MAP: app[inp] = log2-sum over the 16 states of alpha + gamma + beta,
+        // regrouped: u = alpha[s] + beta[next(s, c)] per input class c, summed per
+        // parity pair wy over its 4 states (V), then the 4 branch metrics of the
+        // input on top (the gamma of a branch depends only on the input and wy).
+        float V[2][4];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int wy = 0; wy < 4; ++wy) {
+                float x[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int st = LM_GROUPS.s[c][wy][i];
+                    x[i] = a[st] + b1[t_next(st, c)];
+                }
+                V[c][wy] = lse4(x[0], x[1], x[2], x[3]);
+            }
+        float app[4];
 #pragma unroll
         for (int inp = 0; inp < 4; ++inp) {
-            float t[NS];
+            const int c = (inp == 1 || inp == 2) ? 1 : 0;
+            float y[4];
 #pragma unroll
-            for (int s = 0; s < NS; ++s) t[s] = (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)];
-            app[inp] = lse16(t);
+            for (int wy = 0; wy < 4; ++wy) y[wy] = gam(g, LM_GROUPS.s[c][wy][0], inp) + V[c][wy];
+            app[inp] = lse4(y[0], y[1], y[2], y[3]);
         }
-#else
-#pragma unroll
-        for (int inp = 0; inp < 4; ++inp) app[inp] = acc_first<ALGO>((a[0] + gam(g, 0, inp)) + b1[t_next(0, inp)]);
-#pragma unroll
-        for (int s = 1; s < NS; ++s)
-#pragma unroll
-            for (int inp = 0; inp < 4; ++inp)
-                app[inp] = acc<ALGO>(app[inp], (a[s] + gam(g, s, inp)) + b1[t_next(s, inp)]);
-#endif
+        LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
+        LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
     }
-    const float pA0 = star<ALGO>(app[0], app[1]), pA1 = star<ALGO>(app[2], app[3]);
-    const float pB0 = star<ALGO>(app[0], app[2]), pB1 = star<ALGO>(app[1], app[3]);
-    const float LpA = pA0 - pA1, LpB = pB0 - pB1;
-    double x = ((double)LpA - inA) * sf;
-    double y = ((double)LpB - inB) * sf;
+    // bits -> nats (log-MAP), then the reference's f64 tail (:262-281)
+    double x = ((ALGO ? (double)LpA * LM_LN2 : (double)LpA) - inA) * sf;
+    double y = ((ALGO ? (double)LpB * LM_LN2 : (double)LpB) - inB) * sf;
     x = x > 300.0 ? 300.0 : x;
     x = x < -300.0 ? -300.0 : x;
     y = y > 300.0 ? 300.0 : y;
@@ -486,8 +437,8 @@ struct TileIn {
         r.l = at(La, wsrow(la_idx[k], rs) + lane);
         return r;
     }
-    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
-        make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    template <int ALGO> __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
@@ -519,10 +470,10 @@ struct TileInPre {
         r.l = at(P, wsrow(p_idx[k], rs) + lane);
         return r;
     }
-    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+    template <int ALGO> __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
         iA = r.l.x;
         iB = r.l.y;
-        gamma_from_sums(iA, iB, r.v.z, r.v.w, g);
+        gamma_from_sums<ALGO>(iA, iB, r.v.z, r.v.w, g);
     }
     // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
@@ -602,8 +553,8 @@ struct RowIn {
         r.l = make_double2(LaA[k], LaB[k]);
         return r;
     }
-    __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
-        make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    template <int ALGO> __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
 };
 
@@ -706,7 +657,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
     double iAw[W], iBw[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-        in.gamma(raw[j], gw[j], iAw[j], iBw[j]);
+        in.template gamma<ALGO>(raw[j], gw[j], iAw[j], iBw[j]);
         lcA[j] = raw[j].v.x;
         lcB[j] = raw[j].v.y;
     }
@@ -800,7 +751,7 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
         for (int j = 0; j < FG; ++j) {
             if (tail && k0 + j >= N) continue;   // wave-uniform
             double iA, iB;
-            in.gamma(raw[j], g[j], iA, iB);
+            in.template gamma<ALGO>(raw[j], g[j], iA, iB);
         }
         if (k0 + FG < N) {
 #pragma unroll
@@ -863,7 +814,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
                 for (int j = 0; j < W; ++j) {
                     double iA, iB;
-                    in.gamma(raw[j], g[j], iA, iB);
+                    in.template gamma<ALGO>(raw[j], g[j], iA, iB);
                 }
                 if (k0 + W < N) {
 #pragma unroll
@@ -890,7 +841,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) {
                 double iA, iB;
-                in.gamma(raw[j], g[j], iA, iB);
+                in.template gamma<ALGO>(raw[j], g[j], iA, iB);
             }
             const int kn = k0 + W < N ? k0 + W : k0;
 #pragma unroll
@@ -908,7 +859,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
             for (int j = 0; j < W; ++j) {
                 double iA, iB;
-                in.gamma(raw[j], g[j], iA, iB);
+                in.template gamma<ALGO>(raw[j], g[j], iA, iB);
             }
             if (k0 + W < N) {
 #pragma unroll
@@ -1048,7 +999,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     if (!RAG || lenT > 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            in.gamma(rt[j], gw[j], iAw[j], iBw[j]);
+            in.template gamma<ALGO>(rt[j], gw[j], iAw[j], iBw[j]);
             lcA[j] = rt[j].v.x;
             lcB[j] = rt[j].v.y;
         }
@@ -1063,7 +1014,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
         for (int i = 0; i < 4; ++i) {
             float g[8];
             double x, y;
-            in.gamma(in.staged(st, i), g, x, y);
+            in.template gamma<ALGO>(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
         }
 #pragma unroll
@@ -1076,7 +1027,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const Raw r = in.staged(st, j);
-        in.gamma(r, gw[j], iAw[j], iBw[j]);
+        in.template gamma<ALGO>(r, gw[j], iAw[j], iBw[j]);
         lcA[j] = r.v.x;
         lcB[j] = r.v.y;
     }
@@ -1141,7 +1092,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
 #pragma unroll
             for (int j = 0; j < G; ++j) {
                 double iA, iB;
-                in.gamma(raw[j], g[j], iA, iB);
+                in.template gamma<ALGO>(raw[j], g[j], iA, iB);
             }
             if (k0 + G < N) {
 #pragma unroll
@@ -1860,6 +1811,18 @@ __global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsi
         if (!isfinite(re)) re = 1.5f;
         if (!isfinite(im)) im = -0.75f;
         ok = __float_as_uint(cabs_fin<float>(re, im)) == __float_as_uint(cabs_np<float>(re, im));
+    } else if (which == 3) {
+        // log-MAP primitives outside the captured tables: every f32 t >= 48 (bit
+        // patterns 0x42400000 .. 0x7F800000 = +inf, n ignored) gives 0 <= 2^-t <= 2^-39
+        // (256 * 2^-t is absorbed by any sum >= 1 - 2^-23), with 2^-inf = +0; item 0 also
+        // checks NaN -> NaN for both instructions and log2(1) = 0.
+        const float t = __uint_as_float(0x42400000u + (unsigned)i);
+        const float e = hw_exp2(-t);
+        ok = e >= 0.0f && e <= 0x1p-39f && (t != INFINITY || __float_as_uint(e) == 0u);
+        if (i == 0) {
+            const float qn = __uint_as_float(0x7FC00000u);
+            ok = ok && hw_exp2(qn) != hw_exp2(qn) && hw_log2(qn) != hw_log2(qn) && __float_as_uint(hw_log2(1.0f)) == 0u;
+        }
     } else {
         double re = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i));
         double im = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i + 1));
@@ -1870,6 +1833,16 @@ __global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsi
     if (!ok) atomicAdd(bad, 1ull);
     const unsigned long long act = __ballot(1);   // bad[1]: items evaluated (a launch that did not run fails)
     if ((threadIdx.x & (WAVE - 1)) == (unsigned)__ffsll((long long)act) - 1) atomicAdd(bad + 1, (unsigned long long)__popcll(act));
+}
+
+// The log-MAP primitives' exact outputs (test infrastructure: the oracle's
+// tables, oracle/tdec_oracle.c orc_set_trans): out[i] = v_exp_f32(-t) (which 0)
+// or v_log_f32(w) (which 1) of the f32 whose bit pattern is lo + i.
+__global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, long long n, float *out) {
+    const long long i = (long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const float x = __uint_as_float(lo + (unsigned)i);
+    out[i] = which == 0 ? hw_exp2(-x) : hw_log2(x);
 }
 
 // Fused demap -> f32 -> de-puncture planes (the bench path).

@@ -408,3 +408,25 @@ def turbo_decode(llr, N_couples, code_rate, iterations=8, **kw):
         h = c.handle   # created under the lock: one handle per cached codec
     llr = np.asarray(llr)
     return c.decode_batch(llr) if llr.ndim == 2 else c.decode(llr)
+
+
+# ---- log-MAP primitive tables (diagnostics / test infrastructure) ---------------------
+# The build-defined log-MAP evaluates its max* with the gfx950
+# instructions v_exp_f32 / v_log_f32 on bounded f32 grids.  These are the grids
+# and the device's exact outputs on them, for checkers that restate the
+# definition (the oracle's orc_set_trans takes exactly this tuple).
+TRANS_E_LO, TRANS_E_HI = 0x40F00000, 0x42400000    # t in [7.5, 48]: v_exp_f32(-t)
+TRANS_L_LO, TRANS_L_HI = 0x3F000000, 0x41000000    # w in [0.5, 8]:  v_log_f32(w)
+
+
+def capture_trans_tables(device=0):
+    """(etab, e_lo, ltab, l_lo): v_exp_f32(-t) for every f32 t in [7.5, 48] and
+    v_log_f32(w) for every f32 w in [0.5, 8], indexed by bit pattern - lo, as
+    computed by `device` (tdec_selftest_trans)."""
+    L = _n.lib()
+    out = []
+    for which, lo, hi in ((0, TRANS_E_LO, TRANS_E_HI), (1, TRANS_L_LO, TRANS_L_HI)):
+        tab = np.empty(hi - lo + 1, np.float32)
+        _n.check(L.tdec_selftest_trans(int(device), which, lo, tab.size, tab.ctypes.data))
+        out += [tab, lo]
+    return tuple(out)

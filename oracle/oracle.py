@@ -48,8 +48,32 @@ def lib():
         L.orc_demap_c128.argtypes = [_f64p, C.c_long, _f64p, C.c_int, C.c_int, C.c_double, _f64p]
         L.orc_jac.argtypes = [C.c_float, C.c_float]
         L.orc_jac.restype = C.c_float
+        L.orc_lse4.argtypes = [C.c_float] * 4
+        L.orc_lse4.restype = C.c_float
+        L.orc_set_trans.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]
         _lib = L
     return _lib
+
+
+_trans_keep = None
+
+
+def set_trans(tables=None):
+    """Pin the log-MAP primitives E(t) = 2^-t and L(w) = log2(w) to a device's
+    exhaustive tables: tables = (etab f32, e_lo_bits, ltab f32, l_lo_bits) as
+    captured by modulations_amd.dvb_rcs2_turbo.capture_trans_tables(); None
+    restores the correctly rounded primitives."""
+    global _trans_keep
+    L = lib()
+    if tables is None:
+        L.orc_set_trans(None, 0, 0, None, 0, 0)
+        _trans_keep = None
+        return
+    et, elo, lt, llo = tables
+    et = np.ascontiguousarray(et, np.float32)
+    lt = np.ascontiguousarray(lt, np.float32)
+    _trans_keep = (et, lt)
+    L.orc_set_trans(et.ctypes.data, int(elo), et.size, lt.ctypes.data, int(llo), lt.size)
 
 
 def trellis():

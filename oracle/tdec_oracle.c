@@ -92,86 +92,107 @@ void orc_interleaver(int N, const int32_t *params, int32_t *perm, int32_t *inv_s
 
 static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
 
-/* Build-defined log-MAP max* (SURVEY §8 a11): Jacobian logarithm
- * max(a,b) + log1p(exp(-|a-b|)) (the historic _jacobian_log-22 cut it off at
- * |a-b| > 37; here exp itself underflows to 0 past 104).  The correction is DEFINED as the fixed sequence of
- * f32 IEEE operations below -- exp(-d) = 2^-n * 2^-f from x = d*log2(e) (f = x - n
- * exact), a degree-5 polynomial for 2^-f and log1p(e) = e * Q(e) with a degree-7 Q,
- * all as fused multiply-adds
- * (fmaf is correctly rounded everywhere) -- |error| < 2.5e-7 against the real
- * function.  The HIP kernel (modulations_amd/csrc/tdec_kernels.hip, jac_corr)
- * restates it bit for bit instead of depending on two different libms. */
-static inline float exp_neg(float d)   /* exp(-d), 0 <= d <= 150 */
+/* ---------------------------------------------------------------------------
+ * Build-defined log-MAP (round 3).  The reference has no current
+ * log-MAP source; the historic _jacobian_log-22 was max(a,b) + log1p(exp(-|a-b|)).
+ * This build keeps every log-MAP metric in BITS (base-2 logarithms: the branch
+ * metrics are the reference's f64 sums with the weight 0.5 replaced by
+ * 0.5*log2(e); the extrinsic goes back to nats by one f64 multiply by ln 2), so
+ * the Jacobian logarithm is
+ *     max*(a, b) = maxNum(a, b) + log2(1 + 2^-|a - b|),
+ * evaluated with the gfx950 instructions v_exp_f32 (2^x) and v_log_f32 (log2)
+ * on a quantised argument:
+ *     t = |a - b| + 8          (f32: rounds |a - b| to the 2^-20 grid below 8)
+ *     e = E(t) = v_exp_f32(-t) (= 2^-(|a-b|+8))
+ *     w = fmaf(e, 256, 1)      (= 1 + 2^-|a-b|, one rounding)
+ *     max* = maxNum(a, b) + L(w),  L = v_log_f32.
+ * The +8 keeps the instruction's input on a bounded grid (t in [7.5, 48] for
+ * every correction that can change a result), so its exact outputs form a
+ * finite table.  E and L are faithful (within 1 ulp of the correctly rounded
+ * value; tools/mb/trans_char.hip measured 2.2 % / 23 % of inputs 1 ulp off),
+ * not correctly rounded, so this oracle takes them as data: orc_set_trans()
+ * installs the device's exhaustive tables (captured by tdec_selftest_trans and
+ * checked by the GPU tests to lie within 1 ulp of the correctly rounded values);
+ * without tables the correctly rounded values are used (exp2 / log2 in f64,
+ * rounded once), which is what the CPU-only accuracy tests measure.  Outside
+ * the tables the hardware's behaviour is the one the tests check: NaN -> NaN,
+ * E(t) <= 2^-39 for t > 48 (256 e is then absorbed: 1 + 256 e == 1, and a sum
+ * that already holds a term >= 1 - 2^-23 does not change), E(+inf) = 0.
+ *   lse4(x0..x3) = (Mc - 8) + L(S),  M = maxNum of the four, Mc = M + 8,
+ *                  S = fmaf(E(Mc - x_i), 256, S) over i in order from S = 0
+ *   (Mc - 8 is exact: M rounded to the grid of Mc, the shift every term's
+ *   E(Mc - x_i) * 256 = 2^(x_i - (Mc - 8)) was taken against).
+ * Recursions: each state's two parallel branches first, pm = max*(g(lower
+ * input), g(higher input)), then max*(a[p0] + pm, a[p0 + 8] + pm') over the two
+ * predecessors in table order (beta: successor classes {0, 3} then {1, 2}).
+ * Extrinsic: u[s][c] = alpha[s] + beta[next(s, c)] for the input classes
+ * c = {0, 3}, {1, 2}; V[c][wy] = lse4 over the 4 states (in state order) whose
+ * class-c branches carry the parity pair wy = 2W + Y; app[inp] = lse4 over wy
+ * of (gamma_inp(wy) + V[c(inp)][wy]); LpA = max*(app0, app1) - max*(app2, app3),
+ * LpB = max*(app0, app2) - max*(app1, app3) (bits); Le = ((f64)Lp * ln2 - in) * sf
+ * clipped to +-300.  That is the log-MAP sum (np.logaddexp over the states)
+ * regrouped, so it stays within f32 rounding of log-MAP with exact f64 Jacobian
+ * logarithms (tests/test_oracle_golden.py).  The HIP kernel (tdec_kernels.hip)
+ * runs the same operations in the same order.
+ * ------------------------------------------------------------------------- */
+#define LM_C 8.0f                      /* t = |a - b| + LM_C */
+#define LM_SCALE 256.0f                /* 2^LM_C */
+#define LM_K 0x1.71547652b82fep-1      /* 0.5 * log2(e): the branch metrics' half weight in bits */
+#define LM_LN2 0x1.62e42fefa39efp-1    /* ln 2: bits -> nats */
+
+static const float *g_etab, *g_ltab;   /* device tables (orc_set_trans), or NULL */
+static uint32_t g_elo, g_en, g_llo, g_ln;
+
+static inline uint32_t f2u(float x) { uint32_t u; memcpy(&u, &x, 4); return u; }
+
+/* Install the device's exhaustive tables: etab[i] = v_exp_f32(-t) for the f32 t
+ * whose bit pattern is elo + i (i < en), ltab[i] = v_log_f32(w) for the w with
+ * bit pattern llo + i.  NULL tables restore the correctly rounded primitives. */
+void orc_set_trans(const float *etab, uint32_t elo, uint32_t en, const float *ltab, uint32_t llo, uint32_t ln)
 {
-    const float x = d * 0x1.715476p+0f;                     /* d * log2(e) */
-    const int n = (int)x;
-    const float f = x - (float)n;                             /* exact, in [0, 1) */
-    float p = -0x1.f0ca8p-11f;                                /* 2^-f */
-    p = fmaf(p, f, 0x1.2dd26cp-7f);
-    p = fmaf(p, f, -0x1.c503aep-5f);
-    p = fmaf(p, f, 0x1.ebe33ap-3f);
-    p = fmaf(p, f, -0x1.62e3aap-1f);
-    p = fmaf(p, f, 0x1.fffffep-1f);
-    return ldexpf(p, -n);
+    g_etab = etab; g_elo = elo; g_en = etab ? en : 0;
+    g_ltab = ltab; g_llo = llo; g_ln = ltab ? ln : 0;
 }
 
-static inline float log1p_01(float e)   /* log1p(e), e in [0, 1] */
+static inline float E2neg(float t)   /* 2^-t */
 {
-    float q = -0x1.18f998p-7f;                                /* log1p(e) / e */
-    q = fmaf(q, e, 0x1.6a33e2p-5f);
-    q = fmaf(q, e, -0x1.b9c4c8p-4f);
-    q = fmaf(q, e, 0x1.6ba9f2p-3f);
-    q = fmaf(q, e, -0x1.f5c086p-3f);
-    q = fmaf(q, e, 0x1.54bf8p-2f);
-    q = fmaf(q, e, -0x1.fff95p-2f);
-    q = fmaf(q, e, 0x1.fffffap-1f);
-    return q * e;
+    const uint32_t u = f2u(t);
+    if (u - g_elo < g_en) return g_etab[u - g_elo];
+    return (float)exp2(-(double)t);
 }
 
-static inline float jac_corr(float d)   /* log1p(exp(-d)), 0 <= d <= 150 */
+static inline float L2(float w)      /* log2(w) */
 {
-    return log1p_01(exp_neg(d));
+    const uint32_t u = f2u(w);
+    if (u - g_llo < g_ln) return g_ltab[u - g_llo];
+    return (float)log2((double)w);
 }
 
-/* log(S) for a positive normal S: S = 2^k (1 + u), u in [0, 1) exact */
-static inline float log_pos(float S)
+static inline float jac(float a, float b)   /* max* in bits */
 {
-    int32_t bits;
-    memcpy(&bits, &S, 4);
-    const int k = (bits >> 23) - 127;
-    const int32_t mb = (bits & 0x7FFFFF) | 0x3F800000;
-    float m;
-    memcpy(&m, &mb, 4);
-    return fmaf((float)k, 0x1.62e43p-1f, log1p_01(m - 1.0f));
+    const float m = fmaxf(a, b);
+    const float t = fabsf(a - b) + LM_C;
+    const float w = fmaf(E2neg(t), LM_SCALE, 1.0f);
+    return m + L2(w);
 }
 
-/* log-MAP marginal over the 16 states (the extrinsic's app[inp], build-defined):
- * M = max_s t[s] (maxNum), S = sum over s in state order of exp(-min(M - t[s], 150)),
- * app = M + log(S).  Kernel: lse16 in tdec_kernels.hip. */
-static inline float lse16(const float *t)
+static inline float lse4(float x0, float x1, float x2, float x3)
 {
-    float m = t[0];
-    for (int s = 1; s < NS; ++s) m = fmaxf(m, t[s]);
+    const float M = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3));
+    const float Mc = M + LM_C;
     float S = 0.0f;
-    for (int s = 0; s < NS; ++s) S += exp_neg(fminf(m - t[s], 150.0f));
-    return m + log_pos(S);
+    S = fmaf(E2neg(Mc - x0), LM_SCALE, S);
+    S = fmaf(E2neg(Mc - x1), LM_SCALE, S);
+    S = fmaf(E2neg(Mc - x2), LM_SCALE, S);
+    S = fmaf(E2neg(Mc - x3), LM_SCALE, S);
+    return (Mc - LM_C) + L2(S);   /* Mc - 8: exactly the shift the terms were taken against */
 }
 
-/* max*(a, b) = maxNum(a, b) + log1p(exp(-min(|a - b|, 150))): the correction is
- * exactly 0 past |a - b| = 104 (exp underflows); a NaN operand is dropped. */
-static inline float jac(float a, float b)
-{
-    return fmaxf(a, b) + jac_corr(fminf(fabsf(a - b), 150.0f));
-}
+float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy tests (bits) */
+float orc_lse4(float a, float b, float c, float d) { return lse4(a, b, c, d); }
 
-float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy test */
-
-static inline float star(int algo, float a, float b)
-{
-    return algo ? jac(a, b) : (a > b ? a : b);   /* max_star, :32-35 */
-}
-
-/* bcjr_max_log_map, dvb_rcs2_turbo.py:116-281 (algo 0); algo 1 = log-MAP. */
+/* bcjr_max_log_map, dvb_rcs2_turbo.py:116-281 (algo 0); algo 1 = the build's
+ * log-MAP (above): same passes, metrics in bits, max -> max*. */
 void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
               const double *LaA, const double *LaB, const int32_t *tables, double sf, int algo,
               double *LeA, double *LeB)
@@ -180,6 +201,7 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
     float *gamma = (float *)calloc((size_t)N * NS * 4, sizeof(float));
     float *alpha = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
     float *beta = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
+    const double hw = algo ? LM_K : 0.5;   /* branch-metric half weight: nats (reference) or bits */
 
     /* 1. gamma (:127-160): f64 sum in fixed order, stored as f32 */
     for (int k = 0; k < N; ++k) {
@@ -191,10 +213,10 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
                 int bA = (inp >> 1) & 1, bB = inp & 1;
                 int bW = ow[s * 4 + inp], bY = oy[s * 4 + inp];
                 double m = 0.0;
-                m += in_A * (bA == 0 ? 0.5 : -0.5);
-                m += in_B * (bB == 0 ? 0.5 : -0.5);
-                m += (double)par_W * (bW == 0 ? 0.5 : -0.5);
-                m += (double)par_Y * (bY == 0 ? 0.5 : -0.5);
+                m += in_A * (bA == 0 ? hw : -hw);
+                m += in_B * (bB == 0 ? hw : -hw);
+                m += (double)par_W * (bW == 0 ? hw : -hw);
+                m += (double)par_Y * (bY == 0 ? hw : -hw);
                 gamma[((size_t)k * NS + s) * 4 + inp] = (float)m;
             }
     }
@@ -208,17 +230,19 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
             for (int s = 0; s < NS; ++s) ALP(0, s) = ALP(N, s);
         for (int k = 0; k < N; ++k) {
             for (int n = 0; n < NS; ++n) {
-                float mv = (float)NEG_INF_VAL;
+                float mv;
                 if (algo) {
-                    /* log-MAP (build-defined): each predecessor's two parallel
-                     * branches first, max*(gamma(lower input), gamma(higher input)),
-                     * then max* over the predecessors in table order */
-                    for (int idx = 0; idx < 4; idx += 2) {
-                        int p = ps[n * 4 + idx], i0 = pi[n * 4 + idx], i1 = pi[n * 4 + idx + 1];
+                    /* each predecessor's two parallel branches first, then the two
+                     * predecessors in table order */
+                    float t[2];
+                    for (int q = 0; q < 2; ++q) {
+                        int idx = 2 * q, p = ps[n * 4 + idx], i0 = pi[n * 4 + idx], i1 = pi[n * 4 + idx + 1];
                         int lo = i0 < i1 ? i0 : i1, hi = i0 < i1 ? i1 : i0;
-                        mv = jac(mv, ALP(k, p) + jac(GAM(k, p, lo), GAM(k, p, hi)));
+                        t[q] = ALP(k, p) + jac(GAM(k, p, lo), GAM(k, p, hi));
                     }
+                    mv = jac(t[0], t[1]);
                 } else {
+                    mv = (float)NEG_INF_VAL;
                     for (int idx = 0; idx < 4; ++idx) {
                         int p = ps[n * 4 + idx], in = pi[n * 4 + idx];
                         float t = ALP(k, p) + GAM(k, p, in);
@@ -238,12 +262,13 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
             for (int s = 0; s < NS; ++s) BET(N, s) = BET(0, s);
         for (int k = N - 1; k >= 0; --k) {
             for (int s = 0; s < NS; ++s) {
-                float mv = (float)NEG_INF_VAL;
+                float mv;
                 if (algo) {
-                    /* log-MAP: parallel pairs {0, 3} then {1, 2} (same successor each) */
-                    mv = jac(mv, BET(k + 1, nx[s * 4 + 0]) + jac(GAM(k, s, 0), GAM(k, s, 3)));
-                    mv = jac(mv, BET(k + 1, nx[s * 4 + 1]) + jac(GAM(k, s, 1), GAM(k, s, 2)));
+                    /* parallel pairs {0, 3} then {1, 2} (one successor each) */
+                    mv = jac(BET(k + 1, nx[s * 4 + 0]) + jac(GAM(k, s, 0), GAM(k, s, 3)),
+                             BET(k + 1, nx[s * 4 + 1]) + jac(GAM(k, s, 1), GAM(k, s, 2)));
                 } else {
+                    mv = (float)NEG_INF_VAL;
                     for (int inp = 0; inp < 4; ++inp) {
                         int n = nx[s * 4 + inp];
                         float t = BET(k + 1, n) + GAM(k, s, inp);
@@ -259,28 +284,49 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
 
     /* 4. extrinsic (:232-281) */
     for (int k = 0; k < N; ++k) {
-        float app[4] = {(float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL};
+        float LpA, LpB;
         if (algo) {
-            for (int inp = 0; inp < 4; ++inp) {
-                float t[NS];
-                for (int s = 0; s < NS; ++s) t[s] = ALP(k, s) + GAM(k, s, inp) + BET(k + 1, nx[s * 4 + inp]);
-                app[inp] = lse16(t);
+            /* classes c = 0 (inputs 0, 3) and 1 (inputs 1, 2): u = alpha + beta(next),
+             * grouped by the branches' parity pair wy, then the branch metric per input */
+            float V[2][4];
+            int gs[2][4];   /* a state of each (class, wy) group: its gamma is the group's */
+            for (int c = 0; c < 2; ++c) {
+                float x[4][4];
+                int cnt[4] = {0, 0, 0, 0};
+                for (int s = 0; s < NS; ++s) {
+                    int wy = 2 * ow[s * 4 + c] + oy[s * 4 + c];
+                    if (cnt[wy] == 0) gs[c][wy] = s;
+                    x[wy][cnt[wy]++] = ALP(k, s) + BET(k + 1, nx[s * 4 + c]);
+                }
+                for (int wy = 0; wy < 4; ++wy) V[c][wy] = lse4(x[wy][0], x[wy][1], x[wy][2], x[wy][3]);
             }
+            float app[4];
+            for (int inp = 0; inp < 4; ++inp) {
+                int c = (inp == 1 || inp == 2);
+                float y[4];
+                for (int wy = 0; wy < 4; ++wy) y[wy] = GAM(k, gs[c][wy], inp) + V[c][wy];
+                app[inp] = lse4(y[0], y[1], y[2], y[3]);
+            }
+            LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
+            LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
         } else {
+            float app[4] = {(float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL, (float)NEG_INF_VAL};
             for (int s = 0; s < NS; ++s)
                 for (int inp = 0; inp < 4; ++inp) {
                     int n = nx[s * 4 + inp];
                     float metric = ALP(k, s) + GAM(k, s, inp) + BET(k + 1, n);
                     app[inp] = maxlog_acc(app[inp], metric);
                 }
+            float pA0 = app[0] > app[1] ? app[0] : app[1];   /* max_star, :32-35 */
+            float pA1 = app[2] > app[3] ? app[2] : app[3];
+            float pB0 = app[0] > app[2] ? app[0] : app[2];
+            float pB1 = app[1] > app[3] ? app[1] : app[3];
+            LpA = pA0 - pA1;
+            LpB = pB0 - pB1;
         }
-        float pA0 = star(algo, app[0], app[1]);
-        float pA1 = star(algo, app[2], app[3]);
-        float pB0 = star(algo, app[0], app[2]);
-        float pB1 = star(algo, app[1], app[3]);
-        float LpA = pA0 - pA1, LpB = pB0 - pB1;
-        double a = (double)LpA - ((double)LcA[k] + LaA[k]);
-        double b = (double)LpB - ((double)LcB[k] + LaB[k]);
+        /* log-MAP: bits -> nats by one f64 multiply */
+        double a = (algo ? (double)LpA * LM_LN2 : (double)LpA) - ((double)LcA[k] + LaA[k]);
+        double b = (algo ? (double)LpB * LM_LN2 : (double)LpB) - ((double)LcB[k] + LaB[k]);
         a *= sf; b *= sf;
         const double limit = 300.0;
         if (a > limit) a = limit;

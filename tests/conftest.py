@@ -43,3 +43,32 @@ def G_encode():
 @pytest.fixture(scope="session")
 def G_demap():
     return golden("demap")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _oracle_log_map_primitives():
+    """On a GPU box, pin the oracle's log-MAP primitives (2^-t and log2 on their
+    bounded grids, oracle/tdec_oracle.c orc_set_trans) to this device's
+    v_exp_f32 / v_log_f32 outputs, so every log-MAP comparison is bit for bit;
+    tests/test_gpu_logmap.py checks the tables are faithful (within 1 ulp of the
+    correctly rounded values).  Without a GPU the oracle keeps the correctly
+    rounded primitives."""
+    try:
+        import torch
+        gpu = torch.cuda.is_available()
+    except ImportError:
+        gpu = False
+    if not gpu:
+        yield None
+        return
+    from modulations_amd import dvb_rcs2_turbo as M
+    from oracle import oracle as O
+    tabs = M.capture_trans_tables(0)
+    O.set_trans(tabs)
+    yield tabs
+    O.set_trans(None)
+
+
+@pytest.fixture(scope="session")
+def trans_tables(_oracle_log_map_primitives):
+    return _oracle_log_map_primitives

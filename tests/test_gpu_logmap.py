@@ -77,3 +77,56 @@ def test_logmap_full_size_tile_wrap():
     idx = [0, 1, 63, 64, 131_071, 131_072, B // 2, B - 65, B - 1]
     llr = _host_llrs(codec, syms[idx].cpu().numpy(), "8PSK", n0)
     assert np.array_equal(b1[idx].cpu().numpy(), _oracle(codec, llr))
+
+
+# ---- the hardware primitives of the build-defined log-MAP -------------
+def test_trans_tables_are_faithful(trans_tables):
+    """v_exp_f32 / v_log_f32 on the grids the log-MAP feeds them: every output
+    within 1 ulp of the correctly rounded value (exp2 / log2 in f64, rounded
+    once).  These tables are what the oracle uses in the GPU session."""
+    et, elo, lt, llo = trans_tables
+    t = np.arange(elo, elo + et.size, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    cr = np.exp2(-t.astype(np.float64)).astype(np.float32)
+    d = et.view(np.int32).astype(np.int64) - cr.view(np.int32).astype(np.int64)
+    assert np.all(np.abs(d) <= 1) and np.all(np.isfinite(et))
+    e_off = np.mean(d != 0)
+    w = np.arange(llo, llo + lt.size, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    cr = np.log2(w.astype(np.float64)).astype(np.float32)
+    # log2 near 1 is tiny: compare in ulps of the result
+    d = lt.view(np.int32).astype(np.int64) - cr.view(np.int32).astype(np.int64)
+    assert np.all(np.abs(d) <= 1) and lt[(0x3F800000 - llo)] == 0.0
+    print(f"1-ulp outputs: v_exp_f32 {e_off:.3%}, v_log_f32 {np.mean(d != 0):.3%}")
+
+
+def test_trans_outside_tables():
+    """Every f32 t >= 48 gives 0 <= v_exp_f32(-t) <= 2^-39 (so 256 * 2^-t is
+    absorbed wherever the definition adds it), NaN propagates, log2(1) = 0."""
+    import ctypes as C
+    from modulations_amd import _native
+    bad = C.c_longlong(-1)
+    _native.check(_native.lib().tdec_selftest(0, 3, 0, 0, C.byref(bad)))
+    assert bad.value == 0
+
+
+def _logmap_exact(Lc, La, sf, t):
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_oracle_golden import _logmap_f64_exact
+    return _logmap_f64_exact(Lc, La, sf, t)
+
+
+def test_logmap_gpu_siso_within_1e5_of_exact_log_map():
+    """The kernel's log-MAP SISO (hardware primitives) against log-MAP with exact
+    f64 Jacobian logarithms: the north star's 1e-5 (plus two f32 ulps of the
+    block's largest input metric once that exceeds the f32 resolution)."""
+    rng = np.random.default_rng(1)
+    t, _ = O.trellis()
+    for i, (sc, lsc, n) in enumerate(((1, 3, 48), (4, 3, 48), (2, 8, 212), (6, 20, 212), (3, 10, 752), (8, 40, 100))):
+        Lc = (rng.standard_normal((4, 1, n)) * sc).astype(np.float32)
+        La = rng.standard_normal((2, 1, n)) * lsc
+        A, B = M.bcjr_max_log_map_batch(*Lc, *La, *t, n, 0.7, algo="log-map")
+        RA, RB = _logmap_exact(Lc[:, 0], La[:, 0], 0.7, t)
+        big = max(np.max(np.abs(Lc[0, 0] + La[0, 0])), np.max(np.abs(Lc[1, 0] + La[1, 0])))
+        tol = 1e-5 if i < 3 else 1e-5 + 2 * 2.0 ** -23 * big
+        assert max(np.max(np.abs(A[0] - RA)), np.max(np.abs(B[0] - RB))) <= tol, (sc, lsc, n)

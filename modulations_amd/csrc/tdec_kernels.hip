@@ -766,6 +766,40 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
     }
 }
 
+// B1 of log-MAP as a plain beta recursion (no extrinsic, no stores), then B2
+// over the whole block with the extrinsic.  log-MAP's second passes merge with
+// the first late (8PSK r=1/2 at 2 dB, oracle: per 64-codeword wave the last
+// lane merges after 83 % (F2) / 89 % (B2) of N, median lane 27 %; max-log: 29 %),
+// so the provisional extrinsic of B1 is recomputed almost everywhere anyway:
+// one beta-only pass + one full pass does less work than two extrinsic passes.
+template <int ALGO, bool RAG, class In>
+__device__ __forceinline__ void b1_pass(const In &in, int N, float (&b)[NS]) {
+    constexpr int FG = ALGO ? TDEC_FG_LM : TDEC_FG;
+    Raw raw[FG];
+    // groups [k1 - FG, k1) from the top; the lowest may be short (wave-uniform guards)
+#pragma unroll
+    for (int j = 0; j < FG; ++j) raw[j] = in.load(max(N - FG + j, 0));
+    for (int k1 = N; k1 > 0; k1 -= FG) {
+        float g[FG][8];
+#pragma unroll
+        for (int j = 0; j < FG; ++j) {
+            if (k1 - FG + j < 0) continue;   // wave-uniform
+            double iA, iB;
+            in.template gamma<ALGO>(raw[j], g[j], iA, iB);
+        }
+        if (k1 - FG > 0) {
+#pragma unroll
+            for (int j = 0; j < FG; ++j) raw[j] = in.load(max(k1 - 2 * FG + j, 0));
+        }
+#pragma unroll
+        for (int j = FG - 1; j >= 0; --j)
+            if (k1 - FG + j >= 0) beta_step<ALGO>(b, g[j]);
+    }
+}
+#ifndef TDEC_LM_B1_PLAIN
+#define TDEC_LM_B1_PLAIN 1
+#endif
+
 #ifndef TDEC_UNMASK_ML
 #define TDEC_UNMASK_ML 0
 #endif
@@ -879,6 +913,15 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     float b[NS], an[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
+    if constexpr (ALGO != 0 && TDEC_LM_B1_PLAIN) {
+        b1_pass<ALGO, RAG>(in, N, b);   // b = beta1[0] = beta2[N]
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+        load_vec<true>(an, ck, cs, (top / W) * 4, lane);
+        for (int k0 = top; k0 >= 0; k0 -= W)
+            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
+        return;
+    }
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll

@@ -74,6 +74,13 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
  * :534-535), lfinal (nullable) f64[B][2N] = Lc + La + Le1 (:529-530). */
 int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32_t *bits, double *lfinal);
 
+/* Pinned (page-locked) host memory for the host-pointer entry points: copies
+ * from / to it go straight to the DMA engines, where pageable memory is staged
+ * through the runtime's own pinned buffers.  No reference counterpart (numpy
+ * buffers are pageable); DVBRCS2_Turbo.host_buffer() wraps it. */
+int tdec_host_alloc(size_t bytes, void **out);
+void tdec_host_free(void *p);
+
 /* ---- device-pointer, stream-ordered API (what bench.py and multi-GPU use) ---- */
 
 /* Size the workspace for batches of up to max_batch codewords. */

@@ -28,6 +28,7 @@ EXPORTS = (
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
     "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
+    "tdec_host_alloc", "tdec_host_free",
 )
 
 _lib = None
@@ -74,6 +75,9 @@ def _declare(L):
                                         C.c_int, _vp, _vp, _vp]
     L.tdec_selftest.argtypes = [C.c_int, C.c_int, C.c_longlong, C.c_ulonglong, C.POINTER(C.c_longlong)]
     L.tdec_selftest_trans.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_longlong, _vp]
+    L.tdec_host_alloc.argtypes = [C.c_size_t, C.POINTER(_vp)]
+    L.tdec_host_free.argtypes = [_vp]
+    L.tdec_host_free.restype = None
     for name in EXPORTS:
         f = getattr(L, name)
         if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",
@@ -82,7 +86,8 @@ def _declare(L):
                                             "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_demap_batch",
                                             "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev",
                                             "tdec_count_errors_dev", "tdec_reserve_fused", "tdec_fused_available",
-                                            "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans"):
+                                            "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
+                                            "tdec_host_alloc"):
             f.restype = C.c_int
 
 

@@ -223,7 +223,8 @@ struct tdec_ctx {
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
     hipStream_t stream = nullptr;
-    hipStream_t cstream = nullptr;     // copies of the chunked host-pointer path (created on first use)
+    hipStream_t cstream = nullptr;     // uploads of the chunked host-pointer path (created on first use)
+    hipStream_t dstream = nullptr;     // its downloads (a second copy engine direction)
     // Stream ordering of the handle-owned buffers (workspace, planes_own, cons,
     // staging): every call that touches them records done_ev on the stream it
     // ran on; a later call on a different stream waits on it first, so a
@@ -459,6 +460,7 @@ void tdec_destroy(tdec_t *h) {
     h->planes_w.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
+    if (h->dstream) hipStreamDestroy(h->dstream);
     if (h->done_ev) hipEventDestroy(h->done_ev);
     delete h;
 }
@@ -536,7 +538,8 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size
 // candidate slow; seen in 1 of 6 fresh processes) another round of candidates
 // is allocated while the first ones are still held, up to MAX_CANDIDATES and
 // half of the free memory.  Setup cost: a few hundred ms, once per reserve.
-// TDEC_PLACEMENT_PROBE=0 turns it off.
+// Opt-in since round 3 (TDEC_PLACEMENT_PROBE=1; bench.py sets it): by default
+// reserve() allocates only its own workspace.
 constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 16;
 constexpr float FAST_VS_MEDIAN = 0.97f;
 
@@ -551,8 +554,9 @@ static int ensure_ws(tdec_t *h, int waves) {
     // below) and one sink row per wave for the stores the decoder discards
     const size_t aux_off = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
     const size_t total = aux_off + ((size_t)WAVE + row) * sizeof(double2);
+    // opt-in (bench.py turns it on): a library user's reserve() allocates exactly its workspace
     const char *pe = getenv("TDEC_PLACEMENT_PROBE");
-    const bool probe = !(pe && pe[0] == '0') && waves == h->max_waves && total >= (1ul << 30);
+    const bool probe = pe && pe[0] == '1' && waves == h->max_waves && total >= (1ul << 30);
     if (!probe) {
         // measurement knob (placement study): TDEC_WS_ALLOC=contiguous allocates the
         // workspace as one physically contiguous range
@@ -687,13 +691,15 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
 }
 
 // Host-pointer decode in chunks, so device memory stays bounded for any B:
-// by default half the resident-wave capacity (65 536 codewords on MI355X:
-// the path is PCIe-bound, so small chunks that pipeline well beat large ones,
-// 1.21 M vs 0.70 M codewords/s at 262 144); TDEC_HOST_CHUNK overrides it
-// (tests use a small value to exercise the chunk loop).  With several chunks the copies run
-// on a second stream into two alternating buffers, and the next chunk's H2D is
-// issued before this chunk's D2H (which blocks the host for pageable memory),
-// so uploading chunk i+1 overlaps decoding chunk i.
+// by default half the resident-wave capacity (65 536 codewords on MI355X);
+// TDEC_HOST_CHUNK overrides it (tests use a small value to exercise the chunk
+// loop).  Three streams and two alternating device buffers per direction:
+// uploads (h->cstream), decodes (h->stream) and downloads (h->dstream), so the
+// upload of chunk i+1, the decode of chunk i and the download of chunk i-1 run
+// at once (the two PCIe directions and the GPU).  With pageable host memory HIP
+// stages every copy through its own pinned buffer on the CPU, which caps the
+// path at the host's staging rate; host buffers from tdec_host_alloc (or
+// registered by the caller) go straight to the DMA engines.
 struct EventPair {
     hipEvent_t e[2] = {nullptr, nullptr};
     int create() {
@@ -726,42 +732,61 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     if (!rc && lfinal) rc = h->h_lf.ensure(nbuf * bits_c * sizeof(double));
     if (rc) return rc;
     if (nbuf == 2 && !h->cstream) HIPCHK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
-    hipStream_t cs = nbuf == 2 ? h->cstream : h->stream;
-    EventPair up, dec;
+    if (nbuf == 2 && !h->dstream) HIPCHK(hipStreamCreateWithFlags(&h->dstream, hipStreamNonBlocking));
+    hipStream_t us = nbuf == 2 ? h->cstream : h->stream, ds = nbuf == 2 ? h->dstream : h->stream;
+    EventPair up, dec, down;
     // declared after the events, so it is destroyed (drains the streams) before they are
-    DrainOnExit drain{h->stream, cs};
-    if ((rc = up.create()) || (rc = dec.create())) return rc;
+    struct Drain3 {
+        hipStream_t a, b, c;
+        ~Drain3() {
+            for (hipStream_t s : {a, b, c})
+                if (s) hipStreamSynchronize(s);
+        }
+    } drain{h->stream, us != h->stream ? us : nullptr, ds != h->stream ? ds : nullptr};
+    if ((rc = up.create()) || (rc = dec.create()) || (rc = down.create())) return rc;
     float *dl = (float *)h->h_llr.p;
     int32_t *db = (int32_t *)h->h_bits.p;
     double *df = lfinal ? (double *)h->h_lf.p : nullptr;
     auto rows = [&](long i) { return (int)std::min<long>(C, B - i * C); };
-    auto upload = [&](long i) -> int {
-        const int k = (int)(i % nbuf);
-        HIPCHK(hipMemcpyAsync(dl + k * llr_c, llr + i * C * llr_stride, (size_t)rows(i) * llr_stride * sizeof(float),
-                              hipMemcpyHostToDevice, cs));
-        HIPCHK(hipEventRecord(up.e[k], cs));
-        return 0;
-    };
-    if ((rc = upload(0))) return rc;
     for (long i = 0; i < n_chunks; ++i) {
         const int k = (int)(i % nbuf), n = rows(i);
+        // LLR buffer k was last read by decode i-2
+        if (i >= 2) HIPCHK(hipStreamWaitEvent(us, dec.e[k], 0));
+        HIPCHK(hipMemcpyAsync(dl + k * llr_c, llr + i * C * llr_stride, (size_t)n * llr_stride * sizeof(float),
+                              hipMemcpyHostToDevice, us));
+        HIPCHK(hipEventRecord(up.e[k], us));
         HIPCHK(hipStreamWaitEvent(h->stream, up.e[k], 0));
+        if (i >= 2) HIPCHK(hipStreamWaitEvent(h->stream, down.e[k], 0));   // bits buffer k: download i-2 done
         rc = tdec_decode_batch_dev(h, n, dl + k * llr_c, llr_stride, db + k * bits_c, df ? df + k * bits_c : nullptr,
                                    h->stream);
         if (rc) return rc;
         HIPCHK(hipEventRecord(dec.e[k], h->stream));
-        // buffer (i+1) % 2 was last read by decode i-1, whose D2H is already queued on cs
-        if (i + 1 < n_chunks && (rc = upload(i + 1))) return rc;
-        HIPCHK(hipStreamWaitEvent(cs, dec.e[k], 0));
+        HIPCHK(hipStreamWaitEvent(ds, dec.e[k], 0));
         HIPCHK(hipMemcpyAsync(bits + i * C * row_b, db + k * bits_c, (size_t)n * row_b * sizeof(int32_t),
-                              hipMemcpyDeviceToHost, cs));
+                              hipMemcpyDeviceToHost, ds));
         if (lfinal)
             HIPCHK(hipMemcpyAsync(lfinal + i * C * row_b, df + k * bits_c, (size_t)n * row_b * sizeof(double),
-                                  hipMemcpyDeviceToHost, cs));
+                                  hipMemcpyDeviceToHost, ds));
+        HIPCHK(hipEventRecord(down.e[k], ds));
     }
-    HIPCHK(hipStreamSynchronize(cs));
+    HIPCHK(hipStreamSynchronize(ds));
+    HIPCHK(hipStreamSynchronize(us));
     HIPCHK(hipStreamSynchronize(h->stream));
     return 0;
+}
+
+// Pinned host memory for the host-pointer entry points (the DMA engines read and
+// write it directly; pageable memory is staged by the runtime).
+int tdec_host_alloc(size_t bytes, void **out) {
+    if (!out) return fail(TDEC_EINVAL, "null argument");
+    *out = nullptr;
+    if (bytes == 0) return 0;
+    HIPCHK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    return 0;
+}
+
+void tdec_host_free(void *p) {
+    if (p) hipHostFree(p);
 }
 
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,

@@ -191,9 +191,11 @@ class DVBRCS2_Turbo:
             raise ValueError("decode() takes one codeword; use decode_batch for [B, n] input")
         return self.decode_batch(llr[None, :])[0]
 
-    def decode_batch(self, llr, return_lfinal=False):
+    def decode_batch(self, llr, return_lfinal=False, out=None):
         """Decode B codewords: llr [B, >= n_llr] -> int32 [B, 2N]
-        (and L_final f64 [B, 2N] = Lc + La + Le1, :529-530, when asked)."""
+        (and L_final f64 [B, 2N] = Lc + La + Le1, :529-530, when asked).
+        out: optional C-contiguous int32 [B, 2N] array for the bits (e.g. a
+        host_buffer(), which the copies reach without runtime staging)."""
         llr = np.ascontiguousarray(np.asarray(llr, dtype=np.float32))
         if llr.ndim != 2:
             raise ValueError("decode_batch takes a [B, n] array")
@@ -201,11 +203,23 @@ class DVBRCS2_Turbo:
         if llr.shape[1] < h.llr_len:
             raise IndexError(f"index {llr.shape[1]} is out of bounds for axis 0 with size {llr.shape[1]}")
         B = llr.shape[0]
-        bits = np.zeros((B, self.k_info), np.int32)
+        if out is not None:
+            if out.dtype != np.int32 or out.shape != (B, self.k_info) or not out.flags.c_contiguous:
+                raise ValueError("out must be a C-contiguous int32 [B, 2N] array")
+            bits = out
+        else:
+            bits = np.zeros((B, self.k_info), np.int32)
         lf = np.zeros((B, self.k_info)) if return_lfinal else None
         if B:
             h.call("tdec_decode_batch", B, _n.ptr(llr), llr.shape[1], _n.ptr(bits), _n.ptr(lf))
         return (bits, lf) if return_lfinal else bits
+
+    @staticmethod
+    def host_buffer(shape, dtype=np.float32):
+        """An uninitialised page-locked numpy array (tdec_host_alloc): LLR rows or
+        bit rows in such buffers move over PCIe without the runtime's staging
+        copy.  Freed when the array is garbage-collected."""
+        return pinned_empty(shape, dtype)
 
     # -- device-resident API (torch tensors on this codec's GPU) -------------------------
     def reserve(self, max_batch):
@@ -342,6 +356,20 @@ class DVB_RCS2_TurboCodec(DVBRCS2_Turbo):
         self.block_length = block_length
         self.n_iterations = n_iterations
         self.code_rate = self.k_info / self.n_coded
+
+
+def pinned_empty(shape, dtype=np.float32):
+    """Page-locked host numpy array from tdec_host_alloc, freed with its buffer."""
+    import weakref
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    if n == 0:
+        return np.empty(shape, dtype)
+    p = C.c_void_p()
+    _n.check(_n.lib().tdec_host_alloc(n, C.byref(p)))
+    buf = (C.c_char * n).from_address(p.value)
+    weakref.finalize(buf, _n.lib().tdec_host_free, p.value)
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
 
 # ---- module-level functions of the reference ------------------------------------------

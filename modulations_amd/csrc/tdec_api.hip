@@ -17,6 +17,7 @@
 #include "tdec_kernels.hip"
 #include "tdec_workload.hip"
 #include "tdec_spl.hip"
+#include "tdec_lowlat.hip"
 
 using namespace tdec;
 
@@ -222,6 +223,8 @@ struct tdec_ctx {
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
+    DevBuf ll_ws, ll_st;               // low-latency decoder (state per lane): extrinsic planes, alpha / beta stores
+    int ll_cap = 0;                    // codewords the low-latency workspace holds (batches up to ll_cap - 4)
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // uploads of the chunked host-pointer path (created on first use)
     hipStream_t dstream = nullptr;     // its downloads (a second copy engine direction)
@@ -458,6 +461,8 @@ void tdec_destroy(tdec_t *h) {
     h->cons.buf.release();
     h->spl_ck.release();
     h->planes_w.release();
+    h->ll_ws.release();
+    h->ll_st.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->dstream) hipStreamDestroy(h->dstream);
@@ -633,10 +638,38 @@ static int ensure_ws(tdec_t *h, int waves) {
     return 0;
 }
 
+// Batches of at most lowlat_max() codewords (max-log) run the state-per-lane
+// decoder (tdec_lowlat.hip): lower latency per call, 16x the lanes per codeword.
+// TDEC_LOWLAT_MAX overrides the threshold (0 disables it).
+static int lowlat_max(const tdec_t *h) {
+    static const int v = [] {
+        const char *e = getenv("TDEC_LOWLAT_MAX");
+        return e ? std::max(0, atoi(e)) : 256;
+    }();
+    return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
+}
+static bool use_lowlat(const tdec_t *h, int B) { return B <= lowlat_max(h) && B + 4 <= h->ll_cap; }
+
+static int ensure_lowlat(tdec_t *h, int B) {
+    if (B > lowlat_max(h) || B + 4 <= h->ll_cap) return 0;
+    const int cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
+    if (int rc = h->ll_ws.ensure((size_t)cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
+    if (int rc = h->ll_st.ensure((size_t)cap * ll_st_elems(h->N) * sizeof(float))) return rc;
+    h->ll_cap = cap;
+    return 0;
+}
+
 int tdec_reserve(tdec_t *h, int max_batch) {
     if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
     if (max_batch == 0) return 0;
     Guard g(h->device);
+    if (max_batch <= lowlat_max(h)) {   // small batches: the state-per-lane decoder's workspace only
+        if (max_batch + 4 > h->ll_cap || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);
+        int rc = ensure_lowlat(h, max_batch);
+        if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
+        if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
+        return rc;
+    }
     const int want_waves = std::min(n_tiles_of(max_batch), h->max_waves);
     if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);   // regrowth frees
     int rc = ensure_ws(h, want_waves);
@@ -664,10 +697,18 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     if (B == 0) return 0;
     if (!d_planes || !d_bits) return fail(TDEC_EINVAL, "bad decode arguments");
     Guard g(h->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (use_lowlat(h, B)) {
+        if (int rc = order_on(h, st)) return rc;
+        LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal};
+        hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)((B + 3) / 4)), dim3(WAVE), 0, st, a,
+                           (const int *)h->d_perm, (const int *)h->d_inv);
+        HIPCHK(hipGetLastError());
+        return mark_used(h, st);
+    }
     const int tiles = n_tiles_of(B);
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
-    hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};

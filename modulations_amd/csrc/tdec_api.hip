@@ -789,19 +789,29 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     int32_t *db = (int32_t *)h->h_bits.p;
     double *df = lfinal ? (double *)h->h_lf.p : nullptr;
     auto rows = [&](long i) { return (int)std::min<long>(C, B - i * C); };
-    for (long i = 0; i < n_chunks; ++i) {
+    // chunk i: upload into LLR buffer i % 2 (last read by decode i-2), decode into bits
+    // buffer i % 2 (last read by download i-2).  Issue order upload(i+1), decode(i+1)
+    // before download(i): with pageable memory the runtime performs each copy on this
+    // host thread, so the upload of the next chunk overlaps the running decode and the
+    // next decode is queued before the host blocks in the download.
+    auto stage = [&](long i) -> int {
         const int k = (int)(i % nbuf), n = rows(i);
-        // LLR buffer k was last read by decode i-2
         if (i >= 2) HIPCHK(hipStreamWaitEvent(us, dec.e[k], 0));
         HIPCHK(hipMemcpyAsync(dl + k * llr_c, llr + i * C * llr_stride, (size_t)n * llr_stride * sizeof(float),
                               hipMemcpyHostToDevice, us));
         HIPCHK(hipEventRecord(up.e[k], us));
         HIPCHK(hipStreamWaitEvent(h->stream, up.e[k], 0));
-        if (i >= 2) HIPCHK(hipStreamWaitEvent(h->stream, down.e[k], 0));   // bits buffer k: download i-2 done
-        rc = tdec_decode_batch_dev(h, n, dl + k * llr_c, llr_stride, db + k * bits_c, df ? df + k * bits_c : nullptr,
-                                   h->stream);
-        if (rc) return rc;
+        if (i >= 2) HIPCHK(hipStreamWaitEvent(h->stream, down.e[k], 0));
+        if (int r = tdec_decode_batch_dev(h, n, dl + k * llr_c, llr_stride, db + k * bits_c,
+                                          df ? df + k * bits_c : nullptr, h->stream))
+            return r;
         HIPCHK(hipEventRecord(dec.e[k], h->stream));
+        return 0;
+    };
+    if ((rc = stage(0))) return rc;
+    for (long i = 0; i < n_chunks; ++i) {
+        const int k = (int)(i % nbuf), n = rows(i);
+        if (i + 1 < n_chunks && (rc = stage(i + 1))) return rc;
         HIPCHK(hipStreamWaitEvent(ds, dec.e[k], 0));
         HIPCHK(hipMemcpyAsync(bits + i * C * row_b, db + k * bits_c, (size_t)n * row_b * sizeof(int32_t),
                               hipMemcpyDeviceToHost, ds));

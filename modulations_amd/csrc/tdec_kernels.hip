@@ -730,7 +730,9 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 #ifndef TDEC_FG
 #define TDEC_FG 4
 #endif
-template <int ALGO, int W, bool RAG, class In>
+// STORE = false: the recursion alone (log-MAP's F1, whose checkpoints F2 would
+// overwrite almost everywhere: see TDEC_LM_F1_PLAIN).
+template <int ALGO, int W, bool RAG, bool STORE = true, class In>
 __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigned cs, int lane, float (&a)[NS]) {
     // log-MAP: one checkpoint interval per group (its steps are ~10x larger, and
     // the kernel's instruction footprint, not load latency, is what costs)
@@ -760,7 +762,7 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
 #pragma unroll
         for (int j = 0; j < FG; ++j) {
             if (tail && k0 + j >= N) continue;
-            if (j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
+            if (STORE && j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
             alpha_step<ALGO>(a, g[j]);
         }
     }
@@ -799,6 +801,12 @@ __device__ __forceinline__ void b1_pass(const In &in, int N, float (&b)[NS]) {
 #ifndef TDEC_LM_B1_PLAIN
 #define TDEC_LM_B1_PLAIN 1
 #endif
+// log-MAP's F1 likewise: alpha1 without checkpoints, then F2 over the whole block
+// storing every checkpoint (no merge test): fewer bytes (F2 would rewrite 83 % of
+// the checkpoints after reading them for the test) for 17 % more F2 steps.
+#ifndef TDEC_LM_F1_PLAIN
+#define TDEC_LM_F1_PLAIN 1
+#endif
 
 #ifndef TDEC_UNMASK_ML
 #define TDEC_UNMASK_ML 0
@@ -822,6 +830,11 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
     constexpr bool UNMASK = ALGO ? TDEC_UNMASK_LM : TDEC_UNMASK_ML;
+    bool merged = false;
+    if constexpr (ALGO != 0 && TDEC_LM_F1_PLAIN) {
+        f1_pass<ALGO, W, RAG, false>(in, N, ck, cs, lane, a);   // a = alpha1[N] = alpha2[0]
+        f1_pass<ALGO, W, RAG, true>(in, N, ck, cs, lane, a);    // alpha2, every checkpoint
+    } else {
     // F1 (inputs software-pipelined one group of FG steps ahead)
     f1_pass<ALGO, W, RAG>(in, N, ck, cs, lane, a);
     // F2 until merged (a = alpha1[N] = alpha2[0]).  Per lane: once alpha2 ==
@@ -830,7 +843,6 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
     // wave runs until every lane has merged.
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
-    bool merged = false;
     // Two forms of the partial passes F2 / B2 (bit-identical):
     //  masked:   a merged lane issues no loads or stores (fewer bytes; the branch
     //            around them makes the compiler wait for every outstanding load)
@@ -905,6 +917,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
                 if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
     }
+    }   // F1 + F2
     // B1 fused with the provisional extrinsic, then B2 until merged (b =
     // beta1[0] = beta2[N]); per lane as F2: below its merge point a lane's
     // provisional extrinsics are exact, it stops there.  One copy of the window

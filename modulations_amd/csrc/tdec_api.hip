@@ -701,7 +701,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     if (use_lowlat(h, B)) {
         if (int rc = order_on(h, st)) return rc;
         LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal};
-        hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)((B + 3) / 4)), dim3(WAVE), 0, st, a,
+        hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)B), dim3(WAVE), 0, st, a,
                            (const int *)h->d_perm, (const int *)h->d_inv);
         HIPCHK(hipGetLastError());
         return mark_used(h, st);

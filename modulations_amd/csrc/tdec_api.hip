@@ -638,13 +638,15 @@ static int ensure_ws(tdec_t *h, int waves) {
     return 0;
 }
 
-// Batches of at most lowlat_max() codewords (max-log) run the state-per-lane
-// decoder (tdec_lowlat.hip): lower latency per call, 16x the lanes per codeword.
-// TDEC_LOWLAT_MAX overrides the threshold (0 disables it).
+// Batches of at most lowlat_max() codewords (max-log) run the one-codeword-per-
+// wave decoder (tdec_lowlat.hip): lower latency per call.  Measured (N=752 r=1/2,
+// host-pointer call, profiles/r03h_latency.jsonl, r03i_latency_lowlat4096.json):
+// B = 1 5.0 vs 11.1 ms, 256 6.7 vs 13.2 ms, 1024 9.0 vs 13.6 ms for the per-lane
+// decoder.  TDEC_LOWLAT_MAX overrides the threshold (0 disables it).
 static int lowlat_max(const tdec_t *h) {
     static const int v = [] {
         const char *e = getenv("TDEC_LOWLAT_MAX");
-        return e ? std::max(0, atoi(e)) : 256;
+        return e ? std::max(0, atoi(e)) : 1024;
     }();
     return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
 }

@@ -72,3 +72,24 @@ def test_lowlat_device_api_and_iterations():
         torch.cuda.synchronize()
         rb, _ = _oracle(c, llr)
         assert np.array_equal(bits.cpu().numpy(), rb)
+
+
+@pytest.mark.parametrize("n,rate", [(752, "1/3"), (212, "1/3"), (48, "1/3"), (220, "2/3"), (64, "3/4")])
+def test_throughput_decoder_at_small_batches(n, rate):
+    """A handle reserved for a large batch keeps the one-codeword-per-lane decoder
+    for small ones (no low-latency workspace): that kernel against the oracle at
+    ragged tile counts."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(77 + n)
+    c = M.DVBRCS2_Turbo(n, rate)
+    c.reserve(70_000)
+    for B in (1, 5, 67):
+        llr = _llrs(rng, c, B, 2.0, 1.6)
+        bits = torch.empty((B, c.k_info), dtype=torch.int32, device=dev)
+        lf = torch.empty((B, c.k_info), dtype=torch.float64, device=dev)
+        planes = torch.empty(c.planes_bytes(B) // 4, dtype=torch.float32, device=dev)
+        c.depuncture_device(torch.from_numpy(llr).to(dev), planes)
+        c.decode_planes_device(planes, B, bits, lf)       # no reserve(B): the 70 000 workspace
+        torch.cuda.synchronize()
+        rb, rl = _oracle(c, llr)
+        assert np.array_equal(bits.cpu().numpy(), rb) and np.array_equal(lf.cpu().numpy(), rl)

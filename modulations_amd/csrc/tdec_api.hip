@@ -158,6 +158,28 @@ struct ConsCache {
                 s = d[2 * m] == lev[m >> K] && d[2 * m + 1] == lev[L + (m & (L - 1))];
         }
         if (s) d.insert(d.end(), lev.begin(), lev.end());
+        // Gray-labelled uniform PAM per axis (sym_llrs_gray): the level of label a sits
+        // at position a ^ (a >> 1) of the ascending order, spacings equal within 1 %;
+        // then the levels in position order and {x_0, 1/delta} per axis follow
+        if (s) {
+            std::vector<double> pos(2 * L), prm(4);
+            for (int ax = 0; ax < 2 && s; ++ax) {
+                const double *lv = lev.data() + ax * L;
+                for (int a = 0; a < L; ++a) pos[ax * L + (a ^ (a >> 1))] = lv[a];
+                for (int q = 0; q + 1 < L && s; ++q) s = pos[ax * L + q] < pos[ax * L + q + 1] ? s : 0;
+                const double delta = (pos[ax * L + L - 1] - pos[ax * L]) / (L - 1);
+                for (int q = 0; q + 1 < L && s; ++q)
+                    s = std::fabs(pos[ax * L + q + 1] - pos[ax * L + q] - delta) <= 0.01 * delta ? s : 0;
+                prm[2 * ax] = pos[ax * L];
+                prm[2 * ax + 1] = 1.0 / delta;
+            }
+            if (s) {
+                s = 2;
+                d.insert(d.end(), pos.begin(), pos.end());
+                d.insert(d.end(), prm.begin(), prm.end());
+            }
+            else s = 1;
+        }
         std::vector<float> f(d.begin(), d.end());   // exact: an f32 table only meets f32 arithmetic
         if (want_f64) HIPCHK(hipMemcpyAsync(buf.p, d.data(), sizeof(double) * d.size(), hipMemcpyHostToDevice, st));
         else HIPCHK(hipMemcpyAsync(buf.p, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice, st));

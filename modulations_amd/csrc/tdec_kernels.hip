@@ -1551,9 +1551,12 @@ using npm::cabs_np;
 struct DemapCfg {
     int M, div_f32, sign;
     double nv;                 // max(noise_var, 0.005) already applied (:202)
-    int sep;                   // table is a separable square QAM grid: per-axis levels follow the points
+    int sep;                   // 1: separable square QAM grid (per-axis levels follow the points);
+                               // 2: and each axis a Gray-labelled uniform PAM (position-ordered levels follow)
 };
-constexpr int DM_TAB = 512 + 64;   // LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels)
+// LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels in label order; for a
+// Gray-labelled uniform grid, sep == 2, + the levels in position order and 4 parameters)
+constexpr int DM_TAB = 640;
 
 // One LLR from the two per-half minima (:219-225): NaN propagates, then the
 // division by the noise variance, the +-30 clip and the caller's sign.
@@ -1811,8 +1814,85 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
     return true;
 }
 
+// Gray-labelled uniform PAM on each axis (sep == 2, detected on the host: the
+// 16/64/256QAM tables of sdr_modem.py:142-207 / test_sdr_with_coding.py:72-86).
+// The same candidates as the searches above, found arithmetically instead of by
+// scanning the 2^K levels: the nearest level position p from (s - x_0) / delta,
+// validated by the gap to both neighbours; for bit b the positions whose Gray
+// label has that bit form runs of 2 * 2^(K-1-b) (boundaries at 2^(K-1-b) + j *
+// 2^(K-b)), so the nearest position with the other bit value is one of the two
+// positions just outside p's run, and every other one lies farther on the same
+// side (distance grows monotonically away from s by at least delta^2).  With every
+// decisive gap above the tolerance of the largest candidate distance, the argmin
+// of numpy's |s - c|^2 over each bit-half is unique and is the candidate, so the
+// LLRs are the full scan's bit for bit; anything else (non-finite input, near
+// ties, a wrong position estimate) returns false and the caller scans.
+__device__ __forceinline__ int gray_inv(int q, int K) {
+    int a = q;
+    for (int sh = 1; sh < K; ++sh) a ^= q >> sh;
+    return a;
+}
+template <typename T, int BPS>
+__device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    constexpr int K = BPS / 2, L = 1 << K;
+    if (!(isfinite(sr) && isfinite(si))) return false;
+    const T *pos_i = cons + 2 * (1 << BPS) + 2 * L, *pos_q = pos_i + L, *prm = pos_q + L;
+    const T inf = (T)INFINITY;
+    const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
+    int p[2], cb[2][K];
+    T gapmin = inf, dmax = (T)0;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        const T s = ax ? si : sr;
+        const T *pos = ax ? pos_q : pos_i;
+        const T t = fmin(fmax(rint((s - prm[2 * ax]) * prm[2 * ax + 1]), (T)0), (T)(L - 1));
+        const int q = (int)t;
+        const T e0 = s - pos[q], d0 = e0 * e0;
+        const T el = s - pos[q > 0 ? q - 1 : q], er = s - pos[q < L - 1 ? q + 1 : q];
+        const T dl = q > 0 ? el * el : inf, dr = q < L - 1 ? er * er : inf;
+        gapmin = fmin(gapmin, fmin(dl, dr) - d0);
+        dmax = fmax(dmax, fmax(d0, fmax(q > 0 ? dl : (T)0, q < L - 1 ? dr : (T)0)));
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            const int h = 1 << (K - 1 - b);
+            const int start = q < h ? 0 : h + ((q - h) & ~(2 * h - 1));
+            const int end = min(start == 0 ? h : start + 2 * h, L);
+            const bool lv = start > 0, rv = end < L;
+            const T xl = s - pos[lv ? start - 1 : q], xr = s - pos[rv ? end : q];
+            const T dL = lv ? xl * xl : inf, dR = rv ? xr * xr : inf;
+            if (lv && rv) gapmin = fmin(gapmin, fabs(dL - dR));
+            cb[ax][b] = dL <= dR ? start - 1 : end;
+            dmax = fmax(dmax, fmax(lv ? dL : (T)0, rv ? dR : (T)0));
+        }
+        p[ax] = q;
+    }
+    const T tol = eps * (2 * dmax) + tau;
+    if (!(dmax < inf && gapmin > tol)) return false;
+    const T an = cabs_fin<T>(sr - pos_i[p[0]], si - pos_q[p[1]]);
+    const T dn = an * an;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        const int lab = gray_inv(p[ax], K);
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            const int vn = (lab >> (K - 1 - b)) & 1;
+            const T a = ax ? cabs_fin<T>(sr - pos_i[p[0]], si - pos_q[cb[1][b]])
+                           : cabs_fin<T>(sr - pos_i[cb[0][b]], si - pos_q[p[1]]);
+            const T ao = a * a;
+            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
+        }
+    }
+    return true;
+}
+
 template <typename T, int BPS>
 __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+#ifndef TDEC_DM_GRAY
+#define TDEC_DM_GRAY 1
+#endif
+    if constexpr (TDEC_DM_GRAY && BPS >= 4 && BPS % 2 == 0) {
+        if (c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out)) return;
+    }
     if constexpr (BPS >= 8 && BPS % 2 == 0) {
         if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return;
     } else if constexpr (BPS >= 4 && BPS % 2 == 0) {
@@ -1823,7 +1903,7 @@ __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const Demap
 
 // The table (and a separable table's axis levels) into LDS.
 template <typename T, int BPS> __device__ __forceinline__ void load_table(T *cons, const T *cons_g, const DemapCfg &c) {
-    const int n = 2 * c.M + (c.sep ? 2 * (1 << (BPS / 2)) : 0);
+    const int n = 2 * c.M + (c.sep ? 2 * (1 << (BPS / 2)) : 0) + (c.sep == 2 ? 2 * (1 << (BPS / 2)) + 4 : 0);
     for (int i = threadIdx.x; i < n; i += BLOCK) cons[i] = cons_g[i];
 }
 

@@ -177,6 +177,19 @@ struct ConsCache {
                 s = 2;
                 d.insert(d.end(), pos.begin(), pos.end());
                 d.insert(d.end(), prm.begin(), prm.end());
+                // nb[b][p] = {nearest position left of p, right of p} whose label
+                // (the inverse Gray code of the position) differs from p's in bit b
+                // (MSB first); -1 / L when there is none
+                auto lab = [&](int q) { int a = q; for (int sh = 1; sh < K; ++sh) a ^= q >> sh; return a; };
+                for (int b = 0; b < K; ++b)
+                    for (int q = 0; q < L; ++q) {
+                        const int v = (lab(q) >> (K - 1 - b)) & 1;
+                        int lq = q - 1, rq = q + 1;
+                        while (lq >= 0 && ((lab(lq) >> (K - 1 - b)) & 1) == v) --lq;
+                        while (rq < L && ((lab(rq) >> (K - 1 - b)) & 1) == v) ++rq;
+                        d.push_back(lq);
+                        d.push_back(rq);
+                    }
             }
             else s = 1;
         }

@@ -1555,8 +1555,9 @@ struct DemapCfg {
                                // 2: and each axis a Gray-labelled uniform PAM (position-ordered levels follow)
 };
 // LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels in label order; for a
-// Gray-labelled uniform grid, sep == 2, + the levels in position order and 4 parameters)
-constexpr int DM_TAB = 640;
+// uniform grid labelled through gray[], sep == 2, + the levels in position order, 4
+// parameters and the 2 * K * 2^K neighbour positions of sym_llrs_gray)
+constexpr int DM_TAB = 768;
 
 // One LLR from the two per-half minima (:219-225): NaN propagates, then the
 // division by the noise variance, the +-30 clip and the caller's sign.
@@ -1814,19 +1815,21 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
     return true;
 }
 
-// Gray-labelled uniform PAM on each axis (sep == 2, detected on the host: the
-// 16/64/256QAM tables of sdr_modem.py:142-207 / test_sdr_with_coding.py:72-86).
-// The same candidates as the searches above, found arithmetically instead of by
-// scanning the 2^K levels: the nearest level position p from (s - x_0) / delta,
-// validated by the gap to both neighbours; for bit b the positions whose Gray
-// label has that bit form runs of 2 * 2^(K-1-b) (boundaries at 2^(K-1-b) + j *
-// 2^(K-b)), so the nearest position with the other bit value is one of the two
-// positions just outside p's run, and every other one lies farther on the same
-// side (distance grows monotonically away from s by at least delta^2).  With every
-// decisive gap above the tolerance of the largest candidate distance, the argmin
-// of numpy's |s - c|^2 over each bit-half is unique and is the candidate, so the
-// LLRs are the full scan's bit for bit; anything else (non-finite input, near
-// ties, a wrong position estimate) returns false and the caller scans.
+// Uniform PAM on each axis with the reference's labelling (sep == 2, detected on
+// the host: the 16/64/256QAM tables of sdr_modem.py:142-207 and
+// test_sdr_with_coding.py:72-86 put label a at level position gray[a] = a ^ (a >> 1),
+// so the label at position p is the inverse Gray code of p -- adjacent levels can
+// differ in several label bits).  The same candidates as the searches above, found
+// without scanning the 2^K levels: the nearest level position p from
+// (s - x_0) / delta, validated by the gap to both neighbours; for label bit b the
+// positions with the other bit value nearest to s are the first such position left
+// of p and the first right of p (host table nb[b][p] = {left, right}, -1 / L when
+// none): every other one lies farther on the same side, since distance grows
+// away from s by at least delta^2 per position.  With every decisive gap above the
+// tolerance of the largest candidate distance, the argmin of numpy's |s - c|^2 over
+// each bit-half is unique and is the candidate, so the LLRs are the full scan's bit
+// for bit; anything else (non-finite input, near ties, a wrong position estimate)
+// returns false and the caller scans.
 __device__ __forceinline__ int gray_inv(int q, int K) {
     int a = q;
     for (int sh = 1; sh < K; ++sh) a ^= q >> sh;
@@ -1836,7 +1839,7 @@ template <typename T, int BPS>
 __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr int K = BPS / 2, L = 1 << K;
     if (!(isfinite(sr) && isfinite(si))) return false;
-    const T *pos_i = cons + 2 * (1 << BPS) + 2 * L, *pos_q = pos_i + L, *prm = pos_q + L;
+    const T *pos_i = cons + 2 * (1 << BPS) + 2 * L, *pos_q = pos_i + L, *prm = pos_q + L, *nb = prm + 4;
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
     int p[2], cb[2][K];
@@ -1854,14 +1857,12 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
         dmax = fmax(dmax, fmax(d0, fmax(q > 0 ? dl : (T)0, q < L - 1 ? dr : (T)0)));
 #pragma unroll
         for (int b = 0; b < K; ++b) {
-            const int h = 1 << (K - 1 - b);
-            const int start = q < h ? 0 : h + ((q - h) & ~(2 * h - 1));
-            const int end = min(start == 0 ? h : start + 2 * h, L);
-            const bool lv = start > 0, rv = end < L;
-            const T xl = s - pos[lv ? start - 1 : q], xr = s - pos[rv ? end : q];
+            const int lc = (int)nb[(b * L + q) * 2], rc = (int)nb[(b * L + q) * 2 + 1];
+            const bool lv = lc >= 0, rv = rc < L;
+            const T xl = s - pos[lv ? lc : q], xr = s - pos[rv ? rc : q];
             const T dL = lv ? xl * xl : inf, dR = rv ? xr * xr : inf;
             if (lv && rv) gapmin = fmin(gapmin, fabs(dL - dR));
-            cb[ax][b] = dL <= dR ? start - 1 : end;
+            cb[ax][b] = dL <= dR ? lc : rc;
             dmax = fmax(dmax, fmax(lv ? dL : (T)0, rv ? dR : (T)0));
         }
         p[ax] = q;
@@ -1903,7 +1904,8 @@ __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const Demap
 
 // The table (and a separable table's axis levels) into LDS.
 template <typename T, int BPS> __device__ __forceinline__ void load_table(T *cons, const T *cons_g, const DemapCfg &c) {
-    const int n = 2 * c.M + (c.sep ? 2 * (1 << (BPS / 2)) : 0) + (c.sep == 2 ? 2 * (1 << (BPS / 2)) + 4 : 0);
+    constexpr int L = 1 << (BPS / 2);
+    const int n = 2 * c.M + (c.sep ? 2 * L : 0) + (c.sep == 2 ? 2 * L + 4 + 2 * (BPS / 2) * L : 0);
     for (int i = threadIdx.x; i < n; i += BLOCK) cons[i] = cons_g[i];
 }
 

@@ -256,8 +256,6 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, deadline=args.rank_deadline))
 
-    # the decoder's workspace placement probe is opt-in for library users
-    os.environ.setdefault("TDEC_PLACEMENT_PROBE", "1")
     import torch
     from modulations_amd import demap as D
     from modulations_amd import dvb_rcs2_turbo as M

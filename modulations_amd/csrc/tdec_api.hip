@@ -57,6 +57,72 @@ struct DevBuf {
     }
 };
 
+// A device buffer built from physical chunks mapped into one virtual range in a
+// shuffled order (HIP virtual memory management): the physical placement of the
+// decoder workspace is scattered BY CONSTRUCTION instead of by the placement
+// probe's trial allocations (workspace placement).
+struct VmmBuf {
+    void *va = nullptr;
+    size_t size = 0, chunk = 0;
+    std::vector<hipMemGenericAllocationHandle_t> h;
+    int alloc(int device, size_t bytes, size_t chunk_bytes, unsigned seed) {
+        release();
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = device;
+        size_t gran = 0;
+        if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || !gran)
+            return fail(TDEC_EHIP, "hipMemGetAllocationGranularity failed");
+        chunk = (std::max(chunk_bytes, gran) + gran - 1) / gran * gran;
+        const size_t n = (bytes + chunk - 1) / chunk;
+        size = n * chunk;
+        if (hipMemAddressReserve(&va, size, 0, nullptr, 0) != hipSuccess) {
+            va = nullptr;
+            return fail(TDEC_ENOMEM, "hipMemAddressReserve failed");
+        }
+        h.resize(n);
+        std::vector<size_t> order(n);
+        for (size_t i = 0; i < n; ++i) order[i] = i;
+        unsigned long long x = 0x9E3779B97F4A7C15ull ^ seed;   // splitmix shuffle (deterministic)
+        for (size_t i = n; i > 1; --i) {
+            x += 0x9E3779B97F4A7C15ull;
+            unsigned long long z = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            std::swap(order[i - 1], order[z % i]);
+        }
+        for (size_t i = 0; i < n; ++i) {
+            if (hipMemCreate(&h[i], chunk, &prop, 0) != hipSuccess) {
+                h.resize(i);
+                release();
+                return fail(TDEC_ENOMEM, "hipMemCreate failed (decoder workspace)");
+            }
+            if (hipMemMap((char *)va + order[i] * chunk, chunk, 0, h[i], 0) != hipSuccess) {
+                h.resize(i + 1);
+                release();
+                return fail(TDEC_EHIP, "hipMemMap failed");
+            }
+        }
+        hipMemAccessDesc acc{};
+        acc.location = prop.location;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        if (hipMemSetAccess(va, size, &acc, 1) != hipSuccess) {
+            release();
+            return fail(TDEC_EHIP, "hipMemSetAccess failed");
+        }
+        return 0;
+    }
+    void release() {
+        if (va && size) hipMemUnmap(va, size);
+        for (auto &x : h) hipMemRelease(x);
+        h.clear();
+        if (va) hipMemAddressFree(va, size);
+        va = nullptr;
+        size = 0;
+    }
+};
+
 struct Guard {  // select the handle's device for the duration of a call
     int prev = -1;
     explicit Guard(int dev) {
@@ -246,6 +312,7 @@ struct tdec_ctx {
     int32_t *d_used = nullptr;         // [N]: k in the image of perm
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
+    VmmBuf ws_vmm;                     //   or the same as shuffled physical chunks (TDEC_WS_ALLOC=vmm)
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
     int *d_tile_ctr = nullptr;         // the decoders' tile queue counter (zeroed before each launch)
@@ -487,7 +554,9 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_src);
     hipFree(h->d_tile_ctr);
     hipFree(h->d_off);
+    if (h->ws_vmm.va) h->ws.p = nullptr;   // the VMM range is not a hipMalloc pointer
     h->ws.release();
+    h->ws_vmm.release();
     h->planes_own.release();
     h->h_llr.release();
     h->h_bits.release();
@@ -585,6 +654,11 @@ constexpr float FAST_VS_MEDIAN = 0.97f;
 
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
+    if (h->ws_vmm.va) {   // regrowth of a VMM workspace: drop it first (not a hipMalloc pointer)
+        h->ws.p = nullptr;
+        h->ws.cap = 0;
+        h->ws_vmm.release();
+    }
     const size_t MB2 = 2u << 20;
     // rows of waves*64 lanes (+ row_pad): the planes have 3N rows, the checkpoints ck_stride_of / 64
     const size_t row = (size_t)waves * WAVE + h->row_pad;
@@ -594,14 +668,36 @@ static int ensure_ws(tdec_t *h, int waves) {
     // below) and one sink row per wave for the stores the decoder discards
     const size_t aux_off = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
     const size_t total = aux_off + ((size_t)WAVE + row) * sizeof(double2);
-    // opt-in (bench.py turns it on): a library user's reserve() allocates exactly its workspace
+    // The placement probe is opt-in (TDEC_PLACEMENT_PROBE=1): by default a workspace of
+    // >= 1 GiB is built from 64 MiB physical chunks mapped in a shuffled order
+    // (VmmBuf), which places it scattered by construction -- measured as fast as the
+    // probe's best candidate in every fresh process (profiles/r03m/vmm_ab.txt) with
+    // no transient trial allocations.  TDEC_WS_ALLOC=malloc / contiguous are the
+    // measurement alternatives (one hipMalloc / one physically contiguous range).
     const char *pe = getenv("TDEC_PLACEMENT_PROBE");
     const bool probe = pe && pe[0] == '1' && waves == h->max_waves && total >= (1ul << 30);
     if (!probe) {
-        // measurement knob (placement study): TDEC_WS_ALLOC=contiguous allocates the
-        // workspace as one physically contiguous range
         const char *wa = getenv("TDEC_WS_ALLOC");
-        if (wa && !strcmp(wa, "contiguous")) {
+        const bool vmm = wa ? !strcmp(wa, "vmm") : total >= (1ul << 30);
+        if (vmm) {
+            h->ws.release();
+            const char *cm = getenv("TDEC_VMM_CHUNK_MB");
+            const size_t chunk = (size_t)std::max(1, cm ? atoi(cm) : 64) << 20;
+            if (h->ws_vmm.alloc(h->device, total, chunk, 12345u)) {   // no VMM support: one hipMalloc
+                hipGetLastError();
+                if (int rc = h->ws.ensure(total)) return rc;
+                goto placed;
+            }
+            h->ws.p = h->ws_vmm.va;   // not owned by ws (released through ws_vmm)
+            h->ws.cap = total;
+            h->le_p = (double2 *)h->ws.p;
+            h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
+            h->aux_p = (double2 *)((char *)h->ws.p + aux_off);
+            HIPCHK(hipMemsetAsync(h->aux_p, 0, WAVE * sizeof(double2), h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            h->ws_waves = waves;
+            return 0;
+        } else if (wa && !strcmp(wa, "contiguous")) {
             h->ws.release();
             if (hipExtMallocWithFlags(&h->ws.p, total, hipDeviceMallocContiguous) != hipSuccess) {
                 h->ws.p = nullptr;
@@ -664,6 +760,7 @@ static int ensure_ws(tdec_t *h, int waves) {
         h->ws.p = cand[best];
         h->ws.cap = total;
     }
+placed:
     h->le_p = (double2 *)h->ws.p;
     h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
     h->aux_p = (double2 *)((char *)h->ws.p + aux_off);

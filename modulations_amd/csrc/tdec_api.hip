@@ -458,13 +458,13 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     int blocks_per_cu = 0, n_cu = 0;
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks_per_cu, decode_kernel(algo, n_couples % win_of(algo) != 0), BLOCK, 0);
+            &blocks_per_cu, decode_kernel(algo, n_couples % win_of(algo) != 0), DEC_BLOCK, 0);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (e != hipSuccess) {
         tdec_destroy(h);
         return fail(TDEC_EHIP, std::string("tdec_create: ") + hipGetErrorString(e));
     }
-    h->max_waves = std::max(1, blocks_per_cu) * n_cu * WAVES_PER_BLOCK;
+    h->max_waves = std::max(1, blocks_per_cu) * n_cu * DEC_WAVES;
     if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
@@ -474,7 +474,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     // experiment knob: run the persistent decoder on a percentage of the resident waves
     if (const char *pw = getenv("TDEC_WAVES_PCT")) {
         const int pct = std::max(1, std::min(100, atoi(pw)));
-        h->max_waves = std::max(WAVES_PER_BLOCK, h->max_waves * pct / 100 / WAVES_PER_BLOCK * WAVES_PER_BLOCK);
+        h->max_waves = std::max(DEC_WAVES, h->max_waves * pct / 100 / DEC_WAVES * DEC_WAVES);
     }
     *out = h;
     return TDEC_OK;
@@ -515,6 +515,15 @@ void tdec_destroy(tdec_t *h) {
                 end[i] = (t[i][1] - t0) * 1e-5;   // ms at 100 MHz
                 busy += (t[i][1] - t[i][0]) * 1e-5;
                 tmin = std::min(tmin, nt[i]), tmax = std::max(tmax, nt[i]);
+            }
+            if (const char *dump = getenv("TDEC_WAVE_DUMP")) {   // per wave: start, end (ms), tiles, hw ids
+                static unsigned hw[WT_MAX][2];
+                if (FILE *f = fopen(dump, "a"); f && hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_wave_hw), sizeof(hw)) == hipSuccess) {
+                    fprintf(f, "# launch waves=%d\n", n);
+                    for (int i = 0; i < n; ++i)
+                        fprintf(f, "%d %llu %llu %d %u %u\n", i, t[i][0], t[i][1], nt[i], hw[i][0], hw[i][1]);
+                    fclose(f);
+                }
             }
             std::sort(end.begin(), end.end());
             const double span = (t1 - t0) * 1e-5;
@@ -616,12 +625,12 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size
     const int B = waves * WAVE;
     DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used,
                  h->row_pad, (double2 *)(ws + aux_off), nullptr, ck_rows_of(h)};
-    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
     const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
     float best = 1e30f;
     for (int rep = 0; rep < 2; ++rep) {
         hipEventRecord(e0, h->stream);
-        hipLaunchKernelGGL((decode_fn)k, grid, dim3(BLOCK), 0, h->stream, a, (const int *)h->d_perm,
+        hipLaunchKernelGGL((decode_fn)k, grid, dim3(DEC_BLOCK), 0, h->stream, a, (const int *)h->d_perm,
                            (const int *)h->d_inv, (const int *)h->d_used);
         hipEventRecord(e1, h->stream);
         if (hipEventSynchronize(e1) != hipSuccess) return 1e30f;
@@ -847,8 +856,8 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     const int *pm = h->d_perm, *iv = h->d_inv;
-    const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(BLOCK), 0, st,
+    const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
+    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(DEC_BLOCK), 0, st,
                        a, pm, iv, (const int *)h->d_used);
     HIPCHK(hipGetLastError());
     return mark_used(h, st);

@@ -1207,6 +1207,18 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
 // ---- kernels --------------------------------------------------------------------
 constexpr int BLOCK = 256;               // 4 waves; each wave owns one 64-codeword tile at a time
 constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
+// Waves per block of the tile decoders (k_turbo_decode, k_turbo_decode_logmap).
+// The waves of a block are independent (no barrier), so the block size only
+// decides how the dispatcher can spread waves over CUs: with fewer tiles than
+// wave slots (one round, e.g. configs[1]: 1 600 tiles for 2 048 slots) four-wave
+// blocks leave some CUs with 8 waves and others with 4, and the launch lasts as
+// long as the fullest CU (a CU's memory pipeline, not its SIMDs, is what a tile
+// waits on: profiles/r03p/c1_batch_sweep.txt).
+#ifndef TDEC_DEC_WAVES
+#define TDEC_DEC_WAVES 4
+#endif
+constexpr int DEC_WAVES = TDEC_DEC_WAVES;
+constexpr int DEC_BLOCK = DEC_WAVES * WAVE;
 #ifndef TDEC_WIN
 #define TDEC_WIN 4
 #endif
@@ -1226,13 +1238,13 @@ constexpr int WIN_ML = TDEC_WIN_ML;
 #endif
 constexpr int WIN_LM = TDEC_WIN_LM;      // log-MAP turbo decoder's checkpoint interval
 __host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_ML; }
-constexpr int LDS_STAGE1 = WAVES_PER_BLOCK * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
+constexpr int LDS_STAGE1 = DEC_WAVES * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
 constexpr int LDS_STAGE = LDS_STAGE1 * 2;   // double-buffered (siso8)
 // siso8's LDS per block: lv = 2 staging buffers + the checkpoint slots (float4),
-// ll = 2 staging buffers (double2): 80 KiB, two blocks per CU.  The epilogue's
+// ll = 2 staging buffers (double2): 20 KiB per wave, eight waves per CU.  The epilogue's
 // bit-packing words then live in the wave's own first staging slice (idle
 // between tiles) instead of a separate array that would not fit.
-constexpr int LDS_LV = LDS_STAGE + WAVES_PER_BLOCK * 4 * WAVE;
+constexpr int LDS_LV = LDS_STAGE + DEC_WAVES * 4 * WAVE;
 constexpr int EPI_STRIDE_ML = TDEC_WIN_ML == 8 ? 4 * WAVE * 4 : 2 * WAVE;   // uint32 words between waves' epi areas
 
 // The SISO of the tile decoder: siso8 (LDS-staged, checkpoints every 8) for
@@ -1308,7 +1320,31 @@ struct PlanesIn {
 constexpr int WT_MAX = 16384;
 __device__ unsigned long long g_wave_t[WT_MAX][2];
 __device__ int g_wave_tiles[WT_MAX];
+__device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of each wave
 #endif
+
+// Issue priority by progress through the tile (TDEC_PRIO).  The two waves of a
+// SIMD otherwise issue oldest first: with one tile each (a batch of at most one
+// round of tiles, e.g. configs[1]) the older finishes its tile in ~7.7 ms and the
+// younger runs the last ~3 ms alone at the one-wave rate, 10.7 ms in all
+// (profiles/r03p/).  s_setprio 3..0 over the four quarters of the tile's
+// iterations hands the issue slots to whichever wave is behind, so both move
+// through their tiles together.  Same bits; measured (profiles/r03t/, tools/ab.py,
+// both orders): configs[1] 10.6 -> 10.1 ms per 102 400 codewords, 1 M codewords
+// at 752 couples 244.3 -> 238.5 ms, log-MAP unchanged.
+#ifndef TDEC_PRIO
+#define TDEC_PRIO 1
+#endif
+__device__ __forceinline__ void progress_prio(int it, int iters) {
+    if constexpr (TDEC_PRIO) {
+        switch (3 - (4 * it) / iters) {
+        case 3: __builtin_amdgcn_s_setprio(3); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+        }
+    }
+}
 
 template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
@@ -1316,7 +1352,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                                                    float4 *lv, double2 *ll,
                                                    uint32_t *epi, const Pro &pro = Pro{}, int epi_stride = 2 * WAVE) {
     const int lane = threadIdx.x & (WAVE - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
     const int N = p.N;
     const long NW = (long)N * WAVE;
@@ -1350,6 +1386,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         }
         const bool has_next = nxt < p.n_tiles;
         for (int it = 0; it < p.iters; ++it) {
+            progress_prio(it, p.iters);
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
             run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
@@ -1451,6 +1488,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         g_wave_t[wave][0] = wt0;
         g_wave_t[wave][1] = __builtin_amdgcn_s_memrealtime();
         g_wave_tiles[wave] = wtiles;
+        g_wave_hw[wave][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        g_wave_hw[wave][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
     }
 #endif
 }
@@ -1463,7 +1502,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 #define TDEC_ML_WPE 2
 #endif
 template <bool RAG>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
+__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ float4 lv[LDS_LV];
     __shared__ double2 ll[LDS_STAGE];
@@ -1471,7 +1510,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_W
         turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
                                    EPI_STRIDE_ML);
     } else {
-        __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+        __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
         turbo_decode_tiles<0, RAG>(p, perm, inv, used, lv, ll, epi, PlanesIn{p.planes});
     }
 }
@@ -1479,9 +1518,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_W
 #define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
 #endif
 template <bool RAG>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
+__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
-    __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];
+    __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
     turbo_decode_tiles<1, RAG>(p, perm, inv, used, nullptr, nullptr, epi, PlanesIn{p.planes});
 }
 

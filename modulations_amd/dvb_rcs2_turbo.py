@@ -102,15 +102,17 @@ class DVBRCS2_Turbo:
 
     Extra keyword arguments (all optional, defaults reproduce the reference):
       algo       'max-log' (reference) or 'log-map' (build-defined max* with correction)
-      inv_perm   'stable' (default: np.argsort(perm, kind='stable'), host independent),
-                 'numpy' (the reference's np.argsort(perm) evaluated on this host),
-                 or an explicit int array
+      inv_perm   'numpy' (default: the reference's own np.argsort(perm) (:325),
+                 evaluated by this host's numpy, so the reference run on the same
+                 host gets the same de-interleaver and the same bits),
+                 'stable' (np.argsort(perm, kind='stable'): host independent),
+                 'numpy-avx512' (the survey host's result, pinned), or an int array
       interleaver 'reference' (default; the reference's non-bijective perm) or
                  'valid-perm' (a true permutation: never used for parity)
       device     HIP device ordinal
     """
 
-    def __init__(self, N_couples, code_rate, iterations=8, *, algo="max-log", inv_perm="stable",
+    def __init__(self, N_couples, code_rate, iterations=8, *, algo="max-log", inv_perm="numpy",
                  interleaver="reference", device=None):
         self.N = N_couples
         self.k_info = N_couples * 2

@@ -20,7 +20,8 @@ def test_codec_attributes(G_tables):
     c = M.DVBRCS2_Turbo(752, "1/3")
     assert c.k_info == 1504 and c.n_coded == 4512 and c.iterations == 8
     assert np.array_equal(c.perm, G_tables["perm_752"])
-    assert np.array_equal(c.inv_perm, G_tables["inv_stable_752"])
+    assert np.array_equal(c.inv_perm, np.argsort(c.perm).astype(np.int32))   # the reference's :325 on this host
+    assert np.array_equal(M.DVBRCS2_Turbo(752, "1/3", inv_perm="stable").inv_perm, G_tables["inv_stable_752"])
     for k in ("next_state", "out_W", "out_Y", "prev_state", "prev_input"):
         assert np.array_equal(getattr(c, k), G_tables[k])
     assert np.array_equal(c.G_matrix, G_tables["G"])

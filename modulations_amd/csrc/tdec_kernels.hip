@@ -981,16 +981,20 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 
 // Positions kb+3 .. kb of a half window (kb+len-1 .. kb if ragged), alpha[kb]
 // given, midpoint recompute as back_window.
-template <int ALGO, bool RAG, class Out>
+// MID: am (alpha[kb+2]) is given by the caller instead of recomputed from a0.
+template <int ALGO, bool RAG, bool MID = false, class Out>
 __device__ __forceinline__ void window_half(const Out &out, int kb, int len, const float (&a0)[NS],
                                             const float (&gw)[4][8], const double (&iAw)[4], const double (&iBw)[4],
-                                            const float (&lcA)[4], const float (&lcB)[4], float (&b)[NS], double sf) {
+                                            const float (&lcA)[4], const float (&lcB)[4], float (&b)[NS], double sf,
+                                            const float *mid = nullptr) {
     constexpr int H = 2;
     float am[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) am[s] = a0[s];
+    for (int s = 0; s < NS; ++s) am[s] = MID ? mid[s] : a0[s];
+    if constexpr (!MID) {
 #pragma unroll
-    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+        for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+    }
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
         if (RAG && j >= len) continue;       // wave-uniform
@@ -1063,6 +1067,15 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
 #pragma unroll
     for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
     in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
+    // TDEC_KEEP_MID: alpha[k0+2], passed on the way to alpha[k0+4], is kept for
+    // the bottom half's midpoint instead of being recomputed there.  Measured
+    // slower (profiles/r03w/: 250.9 vs 244.2 ms per 1 M codewords, configs[1]
+    // 14.0 vs 10.4 ms): the 16 registers it holds across the top half cost more
+    // than the two alpha steps it saves.
+#ifndef TDEC_KEEP_MID
+#define TDEC_KEEP_MID 0
+#endif
+    float a2[NS];
     if (!RAG || lenT > 0) {
         float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
         ck_read(st.ck, lane, a4);
@@ -1072,6 +1085,10 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             double x, y;
             in.template gamma<ALGO>(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
+            if (TDEC_KEEP_MID && i == 1) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) a2[s] = a4[s];
+            }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
@@ -1095,7 +1112,10 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     // needed at once by the bottom half, so the wait costs nothing.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
-    window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
+    if (TDEC_KEEP_MID && (!RAG || lenT > 0))
+        window_half<ALGO, RAG, true>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf, a2);
+    else
+        window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
 constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16-step grid over the top 256 steps

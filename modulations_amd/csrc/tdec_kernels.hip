@@ -1137,10 +1137,30 @@ __device__ __forceinline__ void pass_mark(unsigned long long &t, int slot) {
 __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
 #endif
 
+// Issue priority (TDEC_PRIO, see progress_prio below): 1 = by progress through
+// the tile; 2 = by pass (forward passes 3, backward 1); 3 = both (first half of
+// the tile: forward 3, backward 2; second half: 1, 0).
+#ifndef TDEC_PRIO
+#define TDEC_PRIO 1
+#endif
+__device__ __forceinline__ void set_prio(int v) {
+    switch (v) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+__device__ __forceinline__ void phase_prio(bool forward, int half_hi) {
+    if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
+    if constexpr (TDEC_PRIO == 3) set_prio(forward ? half_hi : half_hi - 1);
+}
+
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
-                      const LdsStage &lb, const LdsStage &lb1) {
+                      const LdsStage &lb, const LdsStage &lb1, int half_hi = 3) {
     unsigned long long tpass = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    phase_prio(true, half_hi);
     constexpr int G = 4, CK = 8;
     const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
     Raw raw[G];
@@ -1181,6 +1201,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         }
     }
     pass_mark(tpass, 1);
+    phase_prio(false, half_hi);
     // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
     float b[NS];
 #pragma unroll
@@ -1279,14 +1300,14 @@ __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int ck_win_of(int algo) { return cmin(WIN, cmin(win_of(algo), win_unstaged(algo))); }
 template <int ALGO, bool RAG, bool STAGED, class In, class Out>
 __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs,
-                                         int lane, double sf, float4 *lv, double2 *ll) {
+                                         int lane, double sf, float4 *lv, double2 *ll, int half_hi = 3) {
     if constexpr (ALGO == 0 && STAGED) {
         const int w = threadIdx.x >> 6;
         lds_f4 *v = (lds_f4 *)lv;
         lds_d2 *l = (lds_d2 *)ll;
         lds_f4 *slot = v + LDS_STAGE + w * 4 * WAVE;
         siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{v + w * 4 * WAVE, l + w * 4 * WAVE, lane, slot},
-                         LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot});
+                         LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot}, half_hi);
     } else {
         siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
@@ -1352,18 +1373,8 @@ __device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fie
 // through their tiles together.  Same bits; measured (profiles/r03t/, tools/ab.py,
 // both orders): configs[1] 10.6 -> 10.1 ms per 102 400 codewords, 1 M codewords
 // at 752 couples 244.3 -> 238.5 ms, log-MAP unchanged.
-#ifndef TDEC_PRIO
-#define TDEC_PRIO 1
-#endif
 __device__ __forceinline__ void progress_prio(int it, int iters) {
-    if constexpr (TDEC_PRIO) {
-        switch (3 - (4 * it) / iters) {
-        case 3: __builtin_amdgcn_s_setprio(3); break;
-        case 2: __builtin_amdgcn_s_setprio(2); break;
-        case 1: __builtin_amdgcn_s_setprio(1); break;
-        default: __builtin_amdgcn_s_setprio(0); break;
-        }
-    }
+    if constexpr (TDEC_PRIO == 1) set_prio(3 - (4 * it) / iters);
 }
 
 template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
@@ -1409,13 +1420,13 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             progress_prio(it, p.iters);
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
+            const int half_hi = 2 * it < p.iters ? 3 : 1;
             run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
-                                lv, ll);
+                                lv, ll, half_hi);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
-                                        sf,
-                                lv, ll);
+                                        sf, lv, ll, half_hi);
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
         unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;

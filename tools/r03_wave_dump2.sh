@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r03y; mkdir -p $O
+L=modulations_amd/lib
+TDEC_WAVE_DUMP=$O/c1.txt timeout -k 10 200 python tools/wave_dump.py $L/libtdec_wt4.so --batch 102400 > $O/c1.log 2>&1 || exit $?
+grep -v amdgpu.ids $O/c1.log

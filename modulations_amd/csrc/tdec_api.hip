@@ -302,6 +302,7 @@ const void *decode_kernel(int algo, bool ragged) {
 
 }  // namespace
 
+constexpr size_t SIMD_PROG_BYTES = sizeof(int) * 8192 * 16;   // [XCC, SE, SH, CU, SIMD] key x 16 wave slots
 struct tdec_ctx {
     int device = 0, N = 0, period = 1, iters = 8, algo = 0;
     uint8_t punct[16] = {0};
@@ -316,6 +317,7 @@ struct tdec_ctx {
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
     int *d_tile_ctr = nullptr;         // the decoders' tile queue counter (zeroed before each launch)
+    int *d_simd_prog = nullptr;        // TDEC_PRIO 4 builds: per-SIMD progress slots (zeroed before each launch)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
     int row_pad = 0;   // TDEC_ROW_PAD (placement study): lanes of padding per workspace row
@@ -448,6 +450,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
+    if (e == hipSuccess && TDEC_PRIO == 4) e = hipMalloc(&h->d_simd_prog, SIMD_PROG_BYTES);
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
     if (e == hipSuccess) e = hipMemcpy(h->d_off, off.data(), sizeof(int32_t) * (N + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_perm, perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
@@ -562,6 +565,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_inv);
     hipFree(h->d_src);
     hipFree(h->d_tile_ctr);
+    if (h->d_simd_prog) hipFree(h->d_simd_prog);
     hipFree(h->d_off);
     if (h->ws_vmm.va) h->ws.p = nullptr;   // the VMM range is not a hipMalloc pointer
     h->ws.release();
@@ -855,6 +859,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     if (int rc = order_on(h, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
+    if (h->d_simd_prog && hipMemsetAsync(h->d_simd_prog, 0, SIMD_PROG_BYTES, st) == hipSuccess) a.simd_prog = h->d_simd_prog;
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(DEC_BLOCK), 0, st,

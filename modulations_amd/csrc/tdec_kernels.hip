@@ -1139,9 +1139,12 @@ __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
 
 // Issue priority (TDEC_PRIO, see progress_prio below): 1 = by progress through
 // the tile; 2 = by pass (forward passes 3, backward 1); 3 = both (first half of
-// the tile: forward 3, backward 2; second half: 1, 0).
+// the tile: forward 3, backward 2; second half: 1, 0); 4 = against the other
+// wave of the same SIMD: each wave publishes its progress (half SISOs since the
+// launch) in a per-SIMD table indexed by HW_ID / XCC_ID and issues first while
+// it is behind.
 #ifndef TDEC_PRIO
-#define TDEC_PRIO 1
+#define TDEC_PRIO 4
 #endif
 __device__ __forceinline__ void set_prio(int v) {
     switch (v) {
@@ -1151,16 +1154,35 @@ __device__ __forceinline__ void set_prio(int v) {
     default: __builtin_amdgcn_s_setprio(0); break;
     }
 }
-__device__ __forceinline__ void phase_prio(bool forward, int half_hi) {
+struct Prio {
+    int hi = 3;           // TDEC_PRIO 3: this SISO's forward level (3 or 1 by tile half)
+    int *tab = nullptr;   // TDEC_PRIO 4: this SIMD's 16 progress slots (by wave id), or null
+    int me = 0;           // this wave's slot
+    int prog = 0;         // half SISOs completed before this SISO
+};
+__device__ __forceinline__ void mate_prio(const Prio &pr, int v) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) __hip_atomic_store(pr.tab + pr.me, v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int x = lane < 16 ? __hip_atomic_load(pr.tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    if (lane == pr.me) x = 0;
+    int mate = 0;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) mate = max(mate, __builtin_amdgcn_readlane(x, l));
+    set_prio(mate == 0 ? 2 : (v + 1 < mate ? 3 : (v + 1 > mate ? 1 : 2)));
+}
+__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr) {
     if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
-    if constexpr (TDEC_PRIO == 3) set_prio(forward ? half_hi : half_hi - 1);
+    if constexpr (TDEC_PRIO == 3) set_prio(forward ? pr.hi : pr.hi - 1);
+    if constexpr (TDEC_PRIO == 4) {
+        if (pr.tab) mate_prio(pr, pr.prog + (forward ? 0 : 1));
+    }
 }
 
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
-                      const LdsStage &lb, const LdsStage &lb1, int half_hi = 3) {
+                      const LdsStage &lb, const LdsStage &lb1, const Prio &pr = Prio{}) {
     unsigned long long tpass = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    phase_prio(true, half_hi);
+    phase_prio(true, pr);
     constexpr int G = 4, CK = 8;
     const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
     Raw raw[G];
@@ -1201,7 +1223,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         }
     }
     pass_mark(tpass, 1);
-    phase_prio(false, half_hi);
+    phase_prio(false, pr);
     // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
     float b[NS];
 #pragma unroll
@@ -1300,14 +1322,14 @@ __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 __host__ __device__ constexpr int ck_win_of(int algo) { return cmin(WIN, cmin(win_of(algo), win_unstaged(algo))); }
 template <int ALGO, bool RAG, bool STAGED, class In, class Out>
 __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs,
-                                         int lane, double sf, float4 *lv, double2 *ll, int half_hi = 3) {
+                                         int lane, double sf, float4 *lv, double2 *ll, const Prio &pr = Prio{}) {
     if constexpr (ALGO == 0 && STAGED) {
         const int w = threadIdx.x >> 6;
         lds_f4 *v = (lds_f4 *)lv;
         lds_d2 *l = (lds_d2 *)ll;
         lds_f4 *slot = v + LDS_STAGE + w * 4 * WAVE;
         siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{v + w * 4 * WAVE, l + w * 4 * WAVE, lane, slot},
-                         LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot}, half_hi);
+                         LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot}, pr);
     } else {
         siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
@@ -1331,6 +1353,7 @@ struct DecodeArgs {
     double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
     int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
     int ck_rows;             // checkpoint rows before the beta1 ring: ceil(N / ck_win_of(algo))
+    int *simd_prog = nullptr;   // TDEC_PRIO 4: [8192 SIMDs][16 wave slots] progress, zeroed per launch
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1364,15 +1387,19 @@ __device__ int g_wave_tiles[WT_MAX];
 __device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of each wave
 #endif
 
-// Issue priority by progress through the tile (TDEC_PRIO).  The two waves of a
-// SIMD otherwise issue oldest first: with one tile each (a batch of at most one
-// round of tiles, e.g. configs[1]) the older finishes its tile in ~7.7 ms and the
-// younger runs the last ~3 ms alone at the one-wave rate, 10.7 ms in all
-// (profiles/r03p/).  s_setprio 3..0 over the four quarters of the tile's
-// iterations hands the issue slots to whichever wave is behind, so both move
-// through their tiles together.  Same bits; measured (profiles/r03t/, tools/ab.py,
-// both orders): configs[1] 10.6 -> 10.1 ms per 102 400 codewords, 1 M codewords
-// at 752 couples 244.3 -> 238.5 ms, log-MAP unchanged.
+// Issue priority (TDEC_PRIO).  The two waves of a SIMD otherwise issue oldest
+// first: with one tile each (a batch of at most one round of tiles, e.g.
+// configs[1]) the older finishes its tile in ~7.7 ms and the younger runs the
+// last ~3 ms alone at the one-wave rate, 10.7 ms in all (profiles/r03p/).
+// Policy 1, s_setprio 3..0 over the four quarters of the tile's iterations,
+// hands the issue slots to whichever wave is behind by a quarter: configs[1]
+// 10.6 -> 10.1 ms per 102 400 codewords, 1 M codewords at 752 couples 244.3 ->
+// 238.5 ms (profiles/r03t/).  Policy 4 (default) compares against the other
+// wave of the SIMD every half SISO (per-SIMD progress slots, mate_prio above),
+// so the lag is half a SISO instead of a quarter tile: configs[1] 10.15 -> 9.8-9.9
+// ms, 1 M codewords 243.9 -> 237.3 ms against policy 1 (profiles/r03z/, both
+// orders).  Same bits under every policy; policies 2 / 3 (by pass) measured no
+// better than 1 (profiles/r03x/).
 __device__ __forceinline__ void progress_prio(int it, int iters) {
     if constexpr (TDEC_PRIO == 1) set_prio(3 - (4 * it) / iters);
 }
@@ -1401,6 +1428,15 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 #endif
     pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
     pro.publish();
+    Prio pr;
+    if (TDEC_PRIO == 4 && p.simd_prog) {
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+        const unsigned key = ((xcc & 7u) << 10) | (((hw >> 13) & 7u) << 7) | (((hw >> 12) & 1u) << 6) |
+                             (((hw >> 8) & 15u) << 2) | ((hw >> 4) & 3u);
+        pr.tab = p.simd_prog + key * 16;
+        pr.me = (int)(hw & 15u);
+    }
     // Every wave starts with tile `wave`; with a tile counter the next tile is
     // taken from a queue (one atomic per tile from lane 0, issued at the tile's
     // start, consumed at its end), so waves whose codewords take longer (longer
@@ -1420,13 +1456,15 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             progress_prio(it, p.iters);
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            const int half_hi = 2 * it < p.iters ? 3 : 1;
+            pr.hi = 2 * it < p.iters ? 3 : 1;
             run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
-                                lv, ll, half_hi);
+                                lv, ll, pr);
+            pr.prog += 2;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
-                                        sf, lv, ll, half_hi);
+                                        sf, lv, ll, pr);
+            pr.prog += 2;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
         unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
@@ -1514,6 +1552,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         ++wtiles;
 #endif
     }
+    if (TDEC_PRIO == 4 && pr.tab && lane == 0)
+        __hip_atomic_store(pr.tab + pr.me, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if TDEC_WAVE_TIMING
     if (lane == 0 && wave < WT_MAX) {
         g_wave_t[wave][0] = wt0;

@@ -1170,11 +1170,18 @@ __device__ __forceinline__ void mate_prio(const Prio &pr, int v) {
     for (int l = 0; l < 16; ++l) mate = max(mate, __builtin_amdgcn_readlane(x, l));
     set_prio(mate == 0 ? 2 : (v + 1 < mate ? 3 : (v + 1 > mate ? 1 : 2)));
 }
-__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr) {
+// TDEC_PRIO_FINE: policy 4 also compares halfway through B1 and at B2's start
+// (4 progress units per SISO instead of 2).  Measured no better: configs[1]
+// 9.93-9.95 vs 9.91-9.95 ms, 1 M codewords 247.9 vs 243.6 ms (profiles/r03ab/).
+#ifndef TDEC_PRIO_FINE
+#define TDEC_PRIO_FINE 0
+#endif
+constexpr int PRIO_UNITS = TDEC_PRIO_FINE ? 4 : 2;
+__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr, int unit = -1) {
     if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
     if constexpr (TDEC_PRIO == 3) set_prio(forward ? pr.hi : pr.hi - 1);
     if constexpr (TDEC_PRIO == 4) {
-        if (pr.tab) mate_prio(pr, pr.prog + (forward ? 0 : 1));
+        if (pr.tab) mate_prio(pr, pr.prog + (unit >= 0 ? unit : (forward ? 0 : 1)));
     }
 }
 
@@ -1242,6 +1249,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
 #pragma unroll
 #endif
     for (int pass = 0; pass < 2; ++pass) {
+        if (TDEC_PRIO_FINE && pass == 1) phase_prio(false, pr, 3);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             raw[j] = in.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
@@ -1252,6 +1260,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         for (int k0 = top; k0 >= 0; k0 -= CK) {
             const int r = (top - k0) / CK;
             const bool keep = r % RSTEP8 == 0 && r < RING * RSTEP8;
+            if (TDEC_PRIO_FINE && pass == 0 && r == top / (2 * CK)) phase_prio(false, pr, 2);
             if (pass == 0 && keep) store_vec<false>(ring, cs, r / RSTEP8 * 4, lane, b);   // beta1 entering
             if (pass == 1 && keep) {
                 if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane);
@@ -1460,11 +1469,11 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
                                 lv, ll, pr);
-            pr.prog += 2;
+            pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
             run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
                                         sf, lv, ll, pr);
-            pr.prog += 2;
+            pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
         unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;

@@ -820,9 +820,63 @@ __device__ __forceinline__ void b1_pass(const In &in, int N, float (&b)[NS]) {
 constexpr int RING = 16;   // beta1 kept at RING window starts 16 steps apart: the top 256 steps (merge: median 40, max 122)
 __host__ __device__ constexpr int rstep_of(int w) { return w >= 16 ? 1 : 16 / w; }
 
+// Issue priority (TDEC_PRIO, see progress_prio below): 1 = by progress through
+// the tile; 2 = by pass (forward passes 3, backward 1); 3 = both (first half of
+// the tile: forward 3, backward 2; second half: 1, 0); 4 = against the other
+// wave of the same SIMD: each wave publishes its progress (half SISOs since the
+// launch) in a per-SIMD table indexed by HW_ID / XCC_ID and issues first while
+// it is behind.
+#ifndef TDEC_PRIO
+#define TDEC_PRIO 4
+#endif
+__device__ __forceinline__ void set_prio(int v) {
+    switch (v) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+struct Prio {
+    int hi = 3;           // TDEC_PRIO 3: this SISO's forward level (3 or 1 by tile half)
+    int *tab = nullptr;   // TDEC_PRIO 4: this SIMD's 16 progress slots (by wave id), or null
+    int me = 0;           // this wave's slot
+    int prog = 0;         // half SISOs completed before this SISO
+};
+__device__ __forceinline__ void mate_prio(const Prio &pr, int v) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) __hip_atomic_store(pr.tab + pr.me, v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int x = lane < 16 ? __hip_atomic_load(pr.tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    if (lane == pr.me) x = 0;
+    int mate = 0;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) mate = max(mate, __builtin_amdgcn_readlane(x, l));
+    set_prio(mate == 0 ? 2 : (v + 1 < mate ? 3 : (v + 1 > mate ? 1 : 2)));
+}
+// TDEC_PRIO_FINE: policy 4 also compares halfway through B1 and at B2's start
+// (4 progress units per SISO instead of 2).  Measured no better: configs[1]
+// 9.93-9.95 vs 9.91-9.95 ms, 1 M codewords 247.9 vs 243.6 ms (profiles/r03ab/).
+#ifndef TDEC_PRIO_FINE
+#define TDEC_PRIO_FINE 0
+#endif
+constexpr int PRIO_UNITS = TDEC_PRIO_FINE ? 4 : 2;
+__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr, int unit = -1) {
+    if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
+    if constexpr (TDEC_PRIO == 3) set_prio(forward ? pr.hi : pr.hi - 1);
+    if constexpr (TDEC_PRIO == 4) {
+        if (pr.tab) mate_prio(pr, pr.prog + (unit >= 0 ? unit : (forward ? 0 : 1)));
+    }
+}
+
+// TDEC_PRIO_LM: policy 4 in the log-MAP decoder too.  Measured no different at
+// 1 M codewords (533.5 vs 533.7, 535.3 vs 536.3 ms: profiles/r03ac/), so off.
+#ifndef TDEC_PRIO_LM
+#define TDEC_PRIO_LM 0
+#endif
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane,
-                     double sf) {
+                     double sf, const Prio &pr = Prio{}) {
+    if (TDEC_PRIO_LM) phase_prio(true, pr);
     const int top = RAG ? ((N - 1) / W) * W : N - W;   // start of the (possibly short) top window
     constexpr int RSTEP = rstep_of(W);
     Raw raw[W];
@@ -927,6 +981,7 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
     if constexpr (ALGO != 0 && TDEC_LM_B1_PLAIN) {
+        if (TDEC_PRIO_LM) phase_prio(false, pr);
         b1_pass<ALGO, RAG>(in, N, b);   // b = beta1[0] = beta2[N]
 #pragma unroll
         for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
@@ -1137,54 +1192,6 @@ __device__ __forceinline__ void pass_mark(unsigned long long &t, int slot) {
 __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
 #endif
 
-// Issue priority (TDEC_PRIO, see progress_prio below): 1 = by progress through
-// the tile; 2 = by pass (forward passes 3, backward 1); 3 = both (first half of
-// the tile: forward 3, backward 2; second half: 1, 0); 4 = against the other
-// wave of the same SIMD: each wave publishes its progress (half SISOs since the
-// launch) in a per-SIMD table indexed by HW_ID / XCC_ID and issues first while
-// it is behind.
-#ifndef TDEC_PRIO
-#define TDEC_PRIO 4
-#endif
-__device__ __forceinline__ void set_prio(int v) {
-    switch (v) {
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    default: __builtin_amdgcn_s_setprio(0); break;
-    }
-}
-struct Prio {
-    int hi = 3;           // TDEC_PRIO 3: this SISO's forward level (3 or 1 by tile half)
-    int *tab = nullptr;   // TDEC_PRIO 4: this SIMD's 16 progress slots (by wave id), or null
-    int me = 0;           // this wave's slot
-    int prog = 0;         // half SISOs completed before this SISO
-};
-__device__ __forceinline__ void mate_prio(const Prio &pr, int v) {
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) __hip_atomic_store(pr.tab + pr.me, v + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int x = lane < 16 ? __hip_atomic_load(pr.tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    if (lane == pr.me) x = 0;
-    int mate = 0;
-#pragma unroll
-    for (int l = 0; l < 16; ++l) mate = max(mate, __builtin_amdgcn_readlane(x, l));
-    set_prio(mate == 0 ? 2 : (v + 1 < mate ? 3 : (v + 1 > mate ? 1 : 2)));
-}
-// TDEC_PRIO_FINE: policy 4 also compares halfway through B1 and at B2's start
-// (4 progress units per SISO instead of 2).  Measured no better: configs[1]
-// 9.93-9.95 vs 9.91-9.95 ms, 1 M codewords 247.9 vs 243.6 ms (profiles/r03ab/).
-#ifndef TDEC_PRIO_FINE
-#define TDEC_PRIO_FINE 0
-#endif
-constexpr int PRIO_UNITS = TDEC_PRIO_FINE ? 4 : 2;
-__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr, int unit = -1) {
-    if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
-    if constexpr (TDEC_PRIO == 3) set_prio(forward ? pr.hi : pr.hi - 1);
-    if constexpr (TDEC_PRIO == 4) {
-        if (pr.tab) mate_prio(pr, pr.prog + (unit >= 0 ? unit : (forward ? 0 : 1)));
-    }
-}
-
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
                       const LdsStage &lb, const LdsStage &lb1, const Prio &pr = Prio{}) {
@@ -1340,7 +1347,7 @@ __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, fl
         siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{v + w * 4 * WAVE, l + w * 4 * WAVE, lane, slot},
                          LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot}, pr);
     } else {
-        siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf);
+        siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf, pr);
     }
 }
 

@@ -103,6 +103,8 @@ constexpr float LM_C = 8.0f, LM_SCALE = 256.0f;   // t = |a - b| + LM_C, 2^LM_C
 __device__ __forceinline__ float hw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }   // v_exp_f32
 __device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }    // v_log_f32
 
+typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two IEEE f32 ops per lane
+
 __device__ __forceinline__ float jac(float a, float b) {
     const float t = fabsf(a - b) + LM_C;
     const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
@@ -119,6 +121,35 @@ __device__ __forceinline__ float lse4(float x0, float x1, float x2, float x3) {
     S = fmaf(hw_exp2(-(Mc - x2)), LM_SCALE, S);
     S = fmaf(hw_exp2(-(Mc - x3)), LM_SCALE, S);
     return (Mc - LM_C) + hw_log2(S);
+}
+
+// Two independent max* / lse4 as one packed stream (TDEC_LM_PK): the same IEEE
+// operations in the same order per element, so the same bits as jac / lse4,
+// with the subtraction, the fma and the final add (lse4: the shifts, scale,
+// fma chain and final add) issued as VOP3P pairs instead of two instructions
+// each (the transcendentals and maxima have no packed form).  Measured slower
+// (profiles/r03ad/: 149.1 vs 138.1 ms per 262 144 codewords, same bits): forming
+// the register pairs costs ~560 v_mov_b32 and the VOP3P hazards ~160 s_nop, more
+// than the paired operations save; off.
+#ifndef TDEC_LM_PK
+#define TDEC_LM_PK 0
+#endif
+__device__ __forceinline__ f2 jac2(f2 a, f2 b) {
+    const f2 d = a - b;
+    const f2 e = f2{hw_exp2(-(fabsf(d.x) + LM_C)), hw_exp2(-(fabsf(d.y) + LM_C))};
+    const f2 w = __builtin_elementwise_fma(e, f2{LM_SCALE, LM_SCALE}, f2{1.0f, 1.0f});
+    return f2{fmaxf(a.x, b.x), fmaxf(a.y, b.y)} + f2{hw_log2(w.x), hw_log2(w.y)};
+}
+__device__ __forceinline__ f2 lse4x2(f2 x0, f2 x1, f2 x2, f2 x3) {
+    const f2 Mc = f2{fmaxf(fmaxf(x0.x, x1.x), fmaxf(x2.x, x3.x)), fmaxf(fmaxf(x0.y, x1.y), fmaxf(x2.y, x3.y))} +
+                  f2{LM_C, LM_C};
+    const f2 K = f2{LM_SCALE, LM_SCALE};
+    const f2 d0 = Mc - x0, d1 = Mc - x1, d2 = Mc - x2, d3 = Mc - x3;
+    f2 S = f2{hw_exp2(-d0.x), hw_exp2(-d0.y)} * K;
+    S = __builtin_elementwise_fma(f2{hw_exp2(-d1.x), hw_exp2(-d1.y)}, K, S);
+    S = __builtin_elementwise_fma(f2{hw_exp2(-d2.x), hw_exp2(-d2.y)}, K, S);
+    S = __builtin_elementwise_fma(f2{hw_exp2(-d3.x), hw_exp2(-d3.y)}, K, S);
+    return (Mc - f2{LM_C, LM_C}) + f2{hw_log2(S.x), hw_log2(S.y)};
 }
 
 // The extrinsic's state groups: for input class c (0: inputs {0, 3}, 1: {1, 2},
@@ -141,7 +172,6 @@ __host__ __device__ constexpr LmGroups make_lm_groups() {
 constexpr LmGroups LM_GROUPS = make_lm_groups();
 
 // ---- recursions -----------------------------------------------------------------
-typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32: two IEEE f32 adds per lane
 // max-log: the two branches of a parallel pair (inputs 0/3, or 1/2: same A^B, so
 // the same next state, W and Y) leave one state for the same next state, and
 // round-to-nearest is monotone, so  max(f32(m + g), f32(m + g')) == f32(m + max(g, g'))
@@ -160,8 +190,14 @@ __device__ __forceinline__ void pair_max(const float (&g)[8], float (&pm)[2][4])
 __device__ __forceinline__ void pair_jac(const float (&g)[8], float (&pm)[2][4]) {
 #pragma unroll
     for (int wy = 0; wy < 4; ++wy) {
-        pm[0][wy] = jac(g[wy], -g[3 - wy]);
-        pm[1][wy] = jac(g[4 + wy], -g[4 + 3 - wy]);
+        if constexpr (TDEC_LM_PK) {
+            const f2 r = jac2(f2{g[wy], g[4 + wy]}, f2{-g[3 - wy], -g[4 + 3 - wy]});
+            pm[0][wy] = r.x;
+            pm[1][wy] = r.y;
+        } else {
+            pm[0][wy] = jac(g[wy], -g[3 - wy]);
+            pm[1][wy] = jac(g[4 + wy], -g[4 + 3 - wy]);
+        }
     }
 }
 __device__ __forceinline__ float pm_of(const float (&pm)[2][4], int s, int inp) {
@@ -213,9 +249,18 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
     pair_jac(g, pm);
     float na[NS];
 #pragma unroll
-    for (int ns = 0; ns < NS; ++ns) {
-        const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2);
-        na[ns] = jac(a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)), a[p1] + pm_of(pm, p1, t_prev_i(ns, 2)));
+    for (int ns = 0; ns < NS; ns += 2) {
+        const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2), q0 = t_prev_s(ns + 1, 0), q1 = t_prev_s(ns + 1, 2);
+        const float x0 = a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)), y0 = a[p1] + pm_of(pm, p1, t_prev_i(ns, 2));
+        const float x1 = a[q0] + pm_of(pm, q0, t_prev_i(ns + 1, 0)), y1 = a[q1] + pm_of(pm, q1, t_prev_i(ns + 1, 2));
+        if constexpr (TDEC_LM_PK) {
+            const f2 r = jac2(f2{x0, x1}, f2{y0, y1});
+            na[ns] = r.x;
+            na[ns + 1] = r.y;
+        } else {
+            na[ns] = jac(x0, y0);
+            na[ns + 1] = jac(x1, y1);
+        }
     }
     const float norm = na[0];
 #pragma unroll
@@ -248,7 +293,18 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     pair_jac(g, pm);
     float nb[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) nb[s] = jac(b[t_next(s, 0)] + pm_of(pm, s, 0), b[t_next(s, 1)] + pm_of(pm, s, 1));
+    for (int s = 0; s < NS; s += 2) {
+        const float x0 = b[t_next(s, 0)] + pm_of(pm, s, 0), y0 = b[t_next(s, 1)] + pm_of(pm, s, 1);
+        const float x1 = b[t_next(s + 1, 0)] + pm_of(pm, s + 1, 0), y1 = b[t_next(s + 1, 1)] + pm_of(pm, s + 1, 1);
+        if constexpr (TDEC_LM_PK) {
+            const f2 r = jac2(f2{x0, x1}, f2{y0, y1});
+            nb[s] = r.x;
+            nb[s + 1] = r.y;
+        } else {
+            nb[s] = jac(x0, y0);
+            nb[s + 1] = jac(x1, y1);
+        }
+    }
     const float norm = nb[0];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = nb[s] - norm;
@@ -313,26 +369,52 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int wy = 0; wy < 4; ++wy) {
-                float x[4];
+            for (int wy = 0; wy < 4; wy += 2) {
+                float x[2][4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int st = LM_GROUPS.s[c][wy][i];
-                    x[i] = a[st] + b1[t_next(st, c)];
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int st = LM_GROUPS.s[c][wy + h][i];
+                        x[h][i] = a[st] + b1[t_next(st, c)];
+                    }
+                if constexpr (TDEC_LM_PK) {
+                    const f2 r = lse4x2(f2{x[0][0], x[1][0]}, f2{x[0][1], x[1][1]}, f2{x[0][2], x[1][2]},
+                                        f2{x[0][3], x[1][3]});
+                    V[c][wy] = r.x;
+                    V[c][wy + 1] = r.y;
+                } else {
+                    V[c][wy] = lse4(x[0][0], x[0][1], x[0][2], x[0][3]);
+                    V[c][wy + 1] = lse4(x[1][0], x[1][1], x[1][2], x[1][3]);
                 }
-                V[c][wy] = lse4(x[0], x[1], x[2], x[3]);
             }
         float app[4];
 #pragma unroll
-        for (int inp = 0; inp < 4; ++inp) {
-            const int c = (inp == 1 || inp == 2) ? 1 : 0;
-            float y[4];
+        for (int inp = 0; inp < 4; inp += 2) {
+            float y[2][4];
 #pragma unroll
-            for (int wy = 0; wy < 4; ++wy) y[wy] = gam(g, LM_GROUPS.s[c][wy][0], inp) + V[c][wy];
-            app[inp] = lse4(y[0], y[1], y[2], y[3]);
+            for (int h = 0; h < 2; ++h) {
+                const int c = (inp + h == 1 || inp + h == 2) ? 1 : 0;
+#pragma unroll
+                for (int wy = 0; wy < 4; ++wy) y[h][wy] = gam(g, LM_GROUPS.s[c][wy][0], inp + h) + V[c][wy];
+            }
+            if constexpr (TDEC_LM_PK) {
+                const f2 r = lse4x2(f2{y[0][0], y[1][0]}, f2{y[0][1], y[1][1]}, f2{y[0][2], y[1][2]}, f2{y[0][3], y[1][3]});
+                app[inp] = r.x;
+                app[inp + 1] = r.y;
+            } else {
+                app[inp] = lse4(y[0][0], y[0][1], y[0][2], y[0][3]);
+                app[inp + 1] = lse4(y[1][0], y[1][1], y[1][2], y[1][3]);
+            }
         }
-        LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
-        LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
+        if constexpr (TDEC_LM_PK) {
+            const f2 hi = jac2(f2{app[0], app[0]}, f2{app[1], app[2]}), lo = jac2(f2{app[2], app[1]}, f2{app[3], app[3]});
+            LpA = hi.x - lo.x;
+            LpB = hi.y - lo.y;
+        } else {
+            LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
+            LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
+        }
     }
     // bits -> nats (log-MAP), then the reference's f64 tail (:262-281)
     double x = ((ALGO ? (double)LpA * LM_LN2 : (double)LpA) - inA) * sf;

@@ -821,6 +821,36 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
 #ifndef TDEC_FG_LM
 #define TDEC_FG_LM 2
 #endif
+    // TDEC_F1_ROLL = R > 0 (max-log): a rolling prefetch instead of groups: step
+    // j's input slot is refilled with step j + R's input right after its branch
+    // metrics are formed, so every load has R steps of work to land (the grouped
+    // form gives it only the group's alpha steps) and only one step's metrics
+    // are held.
+#ifndef TDEC_F1_ROLL
+#define TDEC_F1_ROLL 0
+#endif
+    if constexpr (ALGO == 0 && TDEC_F1_ROLL > 0) {
+        constexpr int R = TDEC_F1_ROLL > 0 ? TDEC_F1_ROLL : W;
+        static_assert(R % W == 0, "TDEC_F1_ROLL must be a multiple of W");
+        const bool tail = RAG || N % R != 0;
+        Raw raw[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) raw[j] = in.load(tail ? min(j, N - 1) : j);
+        for (int k0 = 0; k0 < N; k0 += R) {
+            const bool more = k0 + R < N;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if (tail && k0 + j >= N) continue;   // wave-uniform
+                float g[8];
+                double iA, iB;
+                in.template gamma<ALGO>(raw[j], g, iA, iB);
+                if (more) raw[j] = in.load(tail ? min(k0 + R + j, N - 1) : k0 + R + j);
+                if (STORE && j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
+                alpha_step<ALGO>(a, g);
+            }
+        }
+        return;
+    }
     constexpr int FGW = ALGO ? TDEC_FG_LM : TDEC_FG;
     constexpr int FG = FGW > W ? FGW : W;   // a multiple of W
     static_assert(FG % W == 0, "FG must be a multiple of W");

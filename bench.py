@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--all-on-device0", action="store_true", help="every rank on GPU 0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--rank-deadline", type=float, default=1800.0,
                     help="--gpus N without torchrun: kill every rank and exit non-zero after this many seconds")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="initialise the process group (and time through its barrier / all-reduce) even for one "
+                    "rank: exercises the RCCL path on a one-GPU box")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="torch.distributed timeout (s) for rendezvous and collectives")
     a = ap.parse_args()
@@ -265,7 +268,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or args.dist_always
     tdist = None
     dev_idx = 0 if args.all_on_device0 else local
     torch.cuda.set_device(dev_idx)

@@ -47,13 +47,14 @@ def batches(count, batch):
 
 
 def reduce_counters(counters, dist=None):
-    """Sum int64 counters over all ranks (in place) when a process group is up."""
-    if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    """Sum int64 counters over all ranks (in place) when a process group is up
+    (one rank included: bench.py --dist-always runs the collective through RCCL)."""
+    if dist is not None and dist.is_available() and dist.is_initialized():
         dist.all_reduce(counters, op=dist.ReduceOp.SUM)
     return counters
 
 
 def reduce_max(value_tensor, dist=None):
-    if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist is not None and dist.is_available() and dist.is_initialized():
         dist.all_reduce(value_tensor, op=dist.ReduceOp.MAX)
     return value_tensor

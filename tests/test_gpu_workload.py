@@ -129,6 +129,22 @@ def test_bench_spawns_ranks_and_matches_single_rank_counters():
     assert two["ber"]["codewords"] == 8192
 
 
+def test_bench_rccl_path_single_rank_under_torchrun():
+    """The driver's multi-GPU launch (torchrun, one rank per GPU, backend nccl = RCCL,
+    init_process_group(device_id=...), barrier, all-reduce of the counters and of the
+    max time) on the one GPU a test box has: one rank with --dist-always.  Counters
+    equal the plain single-process run's."""
+    # (no "--n": torchrun's own parser takes it for an abbreviation of its options)
+    common = ["--steps", "1", "--warmup", "1", "--no-cpu", "--mod", "QPSK", "--ebn0", "1.0", "--batch", "8192"]
+    port = str(28500 + os.getpid() % 1000)
+    rccl = json.loads(_run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                            "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "1",
+                            "--dist-always", *common]).strip().splitlines()[-1])
+    one = json.loads(_run([sys.executable, "bench.py", "--gpus", "1", *common]).strip().splitlines()[-1])
+    assert rccl["n_gpus"] == 1 and rccl["value"] > 0
+    assert rccl["ber"] == one["ber"] and rccl["ber"]["codewords"] == 8192
+
+
 def test_ber_point_independent_of_world_size(tmp_path):
     args = ["-m", "modulations_amd.ber", "--mod", "QPSK", "--couples", "212", "--rate", "1/3", "--ebn0", "0.5",
             "--codewords", "5000", "--batch", "1500", "--seed", "7"]

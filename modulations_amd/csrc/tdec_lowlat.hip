@@ -122,11 +122,19 @@ struct LLRec {
 __device__ __forceinline__ LLRec ll_rec(const SplLane &L, bool beta) {
     return beta ? LLRec{L.sucA, L.sucB, L.pmS0, L.pmS1, L.base} : LLRec{L.srcA, L.srcB, L.pmA, L.pmB, L.base};
 }
+// state 0's value of the lane's 16-lane row: DPP row_newbcast:0 (gfx90a+), no LDS round trip
+#ifndef TDEC_LL_BCAST
+#define TDEC_LL_BCAST 1
+#endif
+__device__ __forceinline__ float row_lane0(float n, int base) {
+    if constexpr (TDEC_LL_BCAST) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));
+    return __shfl(n, base);
+}
 __device__ __forceinline__ float ll_step(float v, const float (&pm)[8], const LLRec &R) {
     const float x = __shfl(v, R.src0) + sel8(pm, R.i0);
     const float y = __shfl(v, R.src1) + sel8(pm, R.i1);
     const float n = fmaxf(fmaxf(NEG, x), y);
-    return n - __shfl(n, R.base);
+    return n - row_lane0(n, R.base);
 }
 
 constexpr int LL_D = 8;   // loads issued this many steps ahead of their use

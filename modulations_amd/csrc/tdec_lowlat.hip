@@ -76,6 +76,10 @@ struct LLIn1 {   // decoder 1: natural order, a-priori Le2[inv_perm[k]] (0 in th
     __device__ __forceinline__ void gamma(const LLRaw &r, float (&g)[8], double &iA, double &iB) const {
         make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
+    __device__ __forceinline__ void sums(const LLRaw &r, double &iA, double &iB) const {
+        iA = (double)r.v.x + r.l.x;   // make_gamma's f64 additions
+        iB = (double)r.v.y + r.l.y;
+    }
 };
 struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516)
     const float2 *Z;
@@ -93,6 +97,10 @@ struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516
         iA = r.l.x;
         iB = r.l.y;
         gamma_from_sums(iA, iB, r.v.z, r.v.w, g);
+    }
+    __device__ __forceinline__ void sums(const LLRaw &r, double &iA, double &iB) const {
+        iA = r.l.x;
+        iB = r.l.y;
     }
 };
 struct LLOut1 {  // P1 = f64(Lc) + Le1 for decoder 2, Le1 itself in the last iteration
@@ -112,6 +120,28 @@ __device__ __forceinline__ void ll_pm(const float (&g)[8], float (&pm)[8]) {
     pair_max(g, p2);
 #pragma unroll
     for (int i = 0; i < 8; ++i) pm[i] = p2[i >> 2][i & 3];
+}
+
+// TDEC_LL_SPREAD: the branch metrics spread over the row instead of all 8 in every
+// lane: lane j forms g[j & 7] only (gamma_from_sums's f64 operations for that
+// element: the same bits), the pair maxima come from the quad partner by one DPP
+// move (pm[t][wy] pairs g[t*4 + wy] with g[t*4 + 3 - wy], lanes j and j ^ 3), and
+// each lane fetches the two pair maxima (extrinsic: the four metrics) it needs
+// with permutes that do not wait on the recursion, instead of selecting them
+// from 8 registers with cndmask chains.
+#ifndef TDEC_LL_SPREAD
+#define TDEC_LL_SPREAD 1
+#endif
+__device__ __forceinline__ float gamma_lane(double inA, double inB, float w, float y, int i) {
+    const double hA = inA * 0.5, hB = inB * 0.5, hW = (double)w * 0.5, hY = (double)y * 0.5;
+    const double l1 = hA + (((i >> 2) & 1) ? -hB : hB);
+    const double l2 = l1 + (((i >> 1) & 1) ? -hW : hW);
+    return (float)(l2 + ((i & 1) ? -hY : hY));
+}
+// pair maximum pm[j & 7] of lane j's row: fmaxf(g[i], -g[i ^ 3]) as pair_max
+__device__ __forceinline__ float pm_lane(float g) {
+    const float o = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(g), 0x1B, 0xF, 0xF, false));   // quad_perm:[3,2,1,0]
+    return fmaxf(g, -o);
 }
 
 // Per-lane constants: group 0 runs alpha (predecessors), group 1 beta (successors),
@@ -135,6 +165,21 @@ __device__ __forceinline__ float ll_step(float v, const float (&pm)[8], const LL
     const float y = __shfl(v, R.src1) + sel8(pm, R.i1);
     const float n = fmaxf(fmaxf(NEG, x), y);
     return n - row_lane0(n, R.base);
+}
+// the same step with the lane's two pair maxima already fetched
+__device__ __forceinline__ float ll_step2(float v, float p0, float p1, const LLRec &R) {
+    const float x = __shfl(v, R.src0) + p0;
+    const float y = __shfl(v, R.src1) + p1;
+    const float n = fmaxf(fmaxf(NEG, x), y);
+    return n - row_lane0(n, R.base);
+}
+template <class In> __device__ __forceinline__ void lane_pms(const In &in, const LLRaw &r, int s, const LLRec &R,
+                                                            float &p0, float &p1) {
+    double iA, iB;
+    in.sums(r, iA, iB);
+    const float pm = pm_lane(gamma_lane(iA, iB, r.v.z, r.v.w, s & 7));
+    p0 = __shfl(pm, R.base + R.i0);
+    p1 = __shfl(pm, R.base + R.i1);
 }
 
 constexpr int LL_D = 8;   // loads issued this many steps ahead of their use
@@ -165,11 +210,19 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             for (int j = 0; j < LL_D; ++j) {
                 const int k = k0 + j;
                 if (k >= N) break;   // uniform
-                in.gamma(r[j], g, iA, iB);
-                r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                ll_pm(g, pm);
-                vst[slot(k)] = v;
-                v = ll_step(v, pm, R);
+                if constexpr (TDEC_LL_SPREAD) {
+                    float p0, p1;
+                    lane_pms(in, r[j], s, R, p0, p1);
+                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
+                    vst[slot(k)] = v;
+                    v = ll_step2(v, p0, p1, R);
+                } else {
+                    in.gamma(r[j], g, iA, iB);
+                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
+                    ll_pm(g, pm);
+                    vst[slot(k)] = v;
+                    v = ll_step(v, pm, R);
+                }
             }
         }
         // pass 2 from alpha1[N] / beta1[0] until the group's vector equals the stored one
@@ -186,12 +239,22 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
                 const int k = k0 + j;
                 if (k >= N) break;
                 if (!merged) merged = group_all(v == c[j], L.base);
-                in.gamma(r[j], g, iA, iB);
-                r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                if (!merged) {
-                    ll_pm(g, pm);
-                    vst[slot(k)] = v;
-                    v = ll_step(v, pm, R);
+                if constexpr (TDEC_LL_SPREAD) {
+                    float p0, p1;
+                    lane_pms(in, r[j], s, R, p0, p1);
+                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
+                    if (!merged) {
+                        vst[slot(k)] = v;
+                        v = ll_step2(v, p0, p1, R);
+                    }
+                } else {
+                    in.gamma(r[j], g, iA, iB);
+                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
+                    if (!merged) {
+                        ll_pm(g, pm);
+                        vst[slot(k)] = v;
+                        v = ll_step(v, pm, R);
+                    }
                 }
             }
         }
@@ -217,11 +280,17 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             if (!__any(k < N)) break;   // the groups run different k: wave-level exit
             float g[8];
             double iA, iB;
-            in.gamma(r[j], g, iA, iB);
+            float gl = 0.0f;
+            if constexpr (TDEC_LL_SPREAD) {
+                in.sums(r[j], iA, iB);
+                gl = gamma_lane(iA, iB, r[j].v.z, r[j].v.w, s & 7);
+            } else {
+                in.gamma(r[j], g, iA, iB);
+            }
             float app[4];
 #pragma unroll
             for (int inp = 0; inp < 4; ++inp) {
-                const float gv = sel8(g, L.gi[inp]);
+                const float gv = TDEC_LL_SPREAD ? __shfl(gl, L.base + L.gi[inp]) : sel8(g, L.gi[inp]);
                 const float t = (av[j] + (L.gn[inp] ? -gv : gv)) + ((inp == 0 || inp == 3) ? bx[j] : by[j]);
                 app[inp] = row_max16(fmaxf(NEG, t));
             }

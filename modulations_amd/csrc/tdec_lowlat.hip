@@ -44,6 +44,21 @@ __device__ __forceinline__ float row_max16(float v) {
     v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xF, 0xF, false)));   // row_ror:1
     return v;
 }
+// four row maxima, their rotation rounds interleaved (each DPP move reads a value
+// written three instructions earlier: no hazard wait states)
+template <int CTL> __device__ __forceinline__ void row_round4(float (&v)[4]) {
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[i]), CTL, 0xF, 0xF, false));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], o[i]);
+}
+__device__ __forceinline__ void row_max16x4(float (&v)[4]) {
+    row_round4<0x128>(v);   // row_ror:8
+    row_round4<0x124>(v);   // row_ror:4
+    row_round4<0x122>(v);   // row_ror:2
+    row_round4<0x121>(v);   // row_ror:1
+}
 // true when all 16 lanes of the calling lane's group have c set (group-uniform)
 __device__ __forceinline__ bool group_all(bool c, int base) {
     const unsigned long long m = __ballot(c);
@@ -292,8 +307,9 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             for (int inp = 0; inp < 4; ++inp) {
                 const float gv = TDEC_LL_SPREAD ? __shfl(gl, L.base + L.gi[inp]) : sel8(g, L.gi[inp]);
                 const float t = (av[j] + (L.gn[inp] ? -gv : gv)) + ((inp == 0 || inp == 3) ? bx[j] : by[j]);
-                app[inp] = row_max16(fmaxf(NEG, t));
+                app[inp] = fmaxf(NEG, t);
             }
+            row_max16x4(app);
             const float pA0 = app[0] > app[1] ? app[0] : app[1], pA1 = app[2] > app[3] ? app[2] : app[3];
             const float pB0 = app[0] > app[2] ? app[0] : app[2], pB1 = app[1] > app[3] ? app[1] : app[3];
             double x = ((double)(pA0 - pA1) - iA) * sf, y = ((double)(pB0 - pB1) - iB) * sf;

@@ -597,6 +597,18 @@ __device__ __forceinline__ void ws_store(float4 &dst, const float4 &v) {
 #ifndef TDEC_P1_ALL
 #define TDEC_P1_ALL 0
 #endif
+// TDEC_SKIP_UNUSED: decoder 1 skips the extrinsic (and the alpha recompute that
+// only feeds it) at positions whose output no one reads; the store still goes
+// (to the sink row), so every path issues the same memory operations.
+#ifndef TDEC_SKIP_UNUSED
+#define TDEC_SKIP_UNUSED 1
+#endif
+#ifndef TDEC_SKIP_MID
+#define TDEC_SKIP_MID 0
+#endif
+#ifndef TDEC_SKIP_MID_LM
+#define TDEC_SKIP_MID_LM 1
+#endif
 // A discarded store goes to the wave's sink row (L2-resident) instead of being
 // skipped: every position issues the same stores, so the count of memory
 // operations between a load and its use is the same on every path and the
@@ -607,6 +619,10 @@ struct TileOutPre {
     unsigned rs;
     const int *__restrict__ used;
     double2 *sink;     // this wave's sink row
+    // Whether anything reads the extrinsic at k: decoder 2 reads only the rows
+    // in perm's image, so before the last iteration (Le null) the extrinsic of the
+    // other 53 % (N = 752) is dead.  Wave-uniform (scalar load).
+    __device__ __forceinline__ bool need(int k) const { return TDEC_SKIP_UNUSED == 0 || TDEC_P1_ALL || Le || used[k]; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
         // wave-uniform row selects (SGPR pairs), then the lane offset
         double2 *rp = (TDEC_P1_ALL || used[k]) ? &at(P, wsrow(k, rs)) : sink;
@@ -620,6 +636,7 @@ struct TileOut {
     double2 *Le;
     int lane;
     unsigned rs;
+    __device__ __forceinline__ bool need(int) const { return true; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
         ws_store(at(Le, wsrow(k, rs) + lane), make_double2(a, b));
     }
@@ -643,6 +660,7 @@ struct RowIn {
 struct RowOut {
     double *A, *B;
     bool active;
+    __device__ __forceinline__ bool need(int) const { return true; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
         if (active) {
             A[k] = a;
@@ -763,23 +781,33 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
     float am[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) am[s] = a0[s];
+    // the midpoint feeds only the extrinsics of positions >= H (log-MAP: one of
+    // its max*-heavy alpha steps per window of 2, skipped where decoder 1's
+    // output at k0 + 1 is dead)
+    bool needm = !(ALGO ? TDEC_SKIP_MID_LM : TDEC_SKIP_MID);
 #pragma unroll
-    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+    for (int j = H; j < W; ++j) needm = needm || out.need(k0 + j);
+    if (needm) {
+#pragma unroll
+        for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+    }
 #pragma unroll
     for (int j = W - 1; j >= 0; --j) {
         if (RAG && j >= len) continue;       // wave-uniform
         __builtin_amdgcn_sched_barrier(0);   // keep the window positions from being interleaved
         const int from = j >= H ? H : 0;
-        float aj[NS];
+        double leA = 0.0, leB = 0.0;
+        if (out.need(k0 + j)) {
+            float aj[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            aj[s] = j >= H ? am[s] : a0[s];
-            asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
+            for (int s = 0; s < NS; ++s) {
+                aj[s] = j >= H ? am[s] : a0[s];
+                asm volatile("" : "+v"(aj[s]));   // opaque copy: stops CSE from re-materialising the window
+            }
+#pragma unroll
+            for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
+            extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         }
-#pragma unroll
-        for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
-        double leA, leB;
-        extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         if (!CMP || active) out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
         beta_step<ALGO>(b, gw[j]);
     }
@@ -1159,8 +1187,11 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 #pragma unroll
     for (int s = 0; s < NS; ++s) am[s] = MID ? mid[s] : a0[s];
     if constexpr (!MID) {
+        // the midpoint feeds only the extrinsics of positions 2 and 3
+        if (!TDEC_SKIP_MID || out.need(kb + 2) || out.need(kb + 3)) {
 #pragma unroll
-        for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+            for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
+        }
     }
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
@@ -1170,16 +1201,18 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 #endif
         if (TDEC_HALF_SB) __builtin_amdgcn_sched_barrier(0);
         const int from = j >= H ? H : 0;
-        float aj[NS];
+        double leA = 0.0, leB = 0.0;
+        if (out.need(kb + j)) {
+            float aj[NS];
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            aj[s] = j >= H ? am[s] : a0[s];
-            asm volatile("" : "+v"(aj[s]));
+            for (int s = 0; s < NS; ++s) {
+                aj[s] = j >= H ? am[s] : a0[s];
+                asm volatile("" : "+v"(aj[s]));
+            }
+#pragma unroll
+            for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
+            extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         }
-#pragma unroll
-        for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
-        double leA, leB;
-        extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         out.store(kb + j, leA, leB, lcA[j], lcB[j]);
         beta_step<ALGO>(b, gw[j]);
     }

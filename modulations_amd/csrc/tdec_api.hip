@@ -311,6 +311,8 @@ struct tdec_ctx {
     int max_waves = 0;                 // resident waves of the decode kernel on this device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
     int32_t *d_used = nullptr;         // [N]: k in the image of perm
+    int32_t *d_ulist = nullptr;        // [n_used]: the k in the image of perm, ascending (low-latency decoder)
+    int n_used = 0;
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
     VmmBuf ws_vmm;                     //   or the same as shuffled physical chunks (TDEC_WS_ALLOC=vmm)
@@ -447,6 +449,12 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     e = hipMalloc(&h->d_perm, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_used, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMemcpy(h->d_used, used.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
+    std::vector<int32_t> ulist;
+    for (int k = 0; k < N; ++k)
+        if (used[k]) ulist.push_back(k);
+    h->n_used = (int)ulist.size();
+    if (e == hipSuccess) e = hipMalloc(&h->d_ulist, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMemcpy(h->d_ulist, ulist.data(), sizeof(int32_t) * ulist.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
@@ -562,6 +570,7 @@ void tdec_destroy(tdec_t *h) {
 #endif
     hipFree(h->d_perm);
     hipFree(h->d_used);
+    hipFree(h->d_ulist);
     hipFree(h->d_inv);
     hipFree(h->d_src);
     hipFree(h->d_tile_ctr);
@@ -847,7 +856,8 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     hipStream_t st = (hipStream_t)stream;
     if (use_lowlat(h, B)) {
         if (int rc = order_on(h, st)) return rc;
-        LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal};
+        LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal,
+                 (const int *)h->d_ulist, h->n_used};
         hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)B), dim3(WAVE), 0, st, a,
                            (const int *)h->d_perm, (const int *)h->d_inv);
         HIPCHK(hipGetLastError());

@@ -607,7 +607,7 @@ __device__ __forceinline__ void ws_store(float4 &dst, const float4 &v) {
 #define TDEC_SKIP_MID 0
 #endif
 #ifndef TDEC_SKIP_MID_LM
-#define TDEC_SKIP_MID_LM 1
+#define TDEC_SKIP_MID_LM 0   // measured neutral (profiles/r03sk/ab3_lm*.log: 130.1-130.7 vs 130.0-130.5 ms)
 #endif
 // A discarded store goes to the wave's sink row (L2-resident) instead of being
 // skipped: every position issues the same stores, so the count of memory

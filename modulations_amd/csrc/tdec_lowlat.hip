@@ -32,6 +32,8 @@ struct LLArgs {
     float *st;             // per codeword [2][N + 1][16]: alpha store, beta store
     int32_t *bits;         // [B][2N]
     double *lfinal;        // [B][2N] or null
+    const int *ulist;      // [n_used]: the positions in perm's image, ascending
+    int n_used;
 };
 __host__ __device__ constexpr long ll_ws_elems(int N) { return 3L * N; }
 __host__ __device__ constexpr long ll_st_elems(int N) { return 2L * (N + 1) * 16; }
@@ -118,8 +120,20 @@ struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516
         iB = r.l.y;
     }
 };
+// The positions whose extrinsic is computed: i -> pos(i), i < count(N).  Before
+// the last iteration decoder 1's output is read only as P1[perm[j]], so only the
+// n_used positions in perm's image (355 of 752) are computed
+// (TDEC_LL_SKIP_UNUSED); otherwise every position.
+#ifndef TDEC_LL_SKIP_UNUSED
+#define TDEC_LL_SKIP_UNUSED 1
+#endif
 struct LLOut1 {  // P1 = f64(Lc) + Le1 for decoder 2, Le1 itself in the last iteration
     double2 *P1, *Le1;
+    const int *ulist;
+    int n_used;
+    __device__ __forceinline__ bool sparse() const { return TDEC_LL_SKIP_UNUSED && !Le1; }
+    __device__ __forceinline__ int count(int N) const { return sparse() ? n_used : N; }
+    __device__ __forceinline__ int pos(int i) const { return sparse() ? ulist[i] : i; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
         P1[k] = make_double2((double)lcA + a, (double)lcB + b);
         if (Le1) Le1[k] = make_double2(a, b);
@@ -127,6 +141,8 @@ struct LLOut1 {  // P1 = f64(Lc) + Le1 for decoder 2, Le1 itself in the last ite
 };
 struct LLOut2 {
     double2 *Le2;
+    __device__ __forceinline__ int count(int N) const { return N; }
+    __device__ __forceinline__ int pos(int i) const { return i; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const { Le2[k] = make_double2(a, b); }
 };
 
@@ -275,15 +291,18 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
         }
     }
     ll_sync();
-    // extrinsic (:232-281) at every position from the stored alpha2[k], beta2[k+1]:
-    // group q takes k = q, q + 4, ...
+    // extrinsic (:232-281) from the stored alpha2[k], beta2[k+1] at every position
+    // anyone reads (out.pos(i), i < M): group q takes i = q, q + 4, ...
     const int nx0 = L.nxt[0], nx1 = L.nxt[1];   // next(s, 0) = next(s, 3), next(s, 1) = next(s, 2)
-    for (int k0 = grp; k0 < N; k0 += 4 * LL_D) {
+    const int M = out.count(N);
+    for (int i0 = grp; i0 < M; i0 += 4 * LL_D) {
         LLRaw r[LL_D];
         float av[LL_D], bx[LL_D], by[LL_D];
+        int kk[LL_D];
 #pragma unroll
         for (int j = 0; j < LL_D; ++j) {
-            const int k = min(k0 + 4 * j, N - 1);
+            const int k = out.pos(min(i0 + 4 * j, M - 1));
+            kk[j] = k;
             r[j] = in.load(k);
             av[j] = ast[k * 16 + s];
             bx[j] = bst[(k + 1) * 16 + nx0];
@@ -291,8 +310,8 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
         }
 #pragma unroll
         for (int j = 0; j < LL_D; ++j) {
-            const int k = k0 + 4 * j;
-            if (!__any(k < N)) break;   // the groups run different k: wave-level exit
+            const int i = i0 + 4 * j, k = kk[j];
+            if (!__any(i < M)) break;   // the groups run different i: wave-level exit
             float g[8];
             double iA, iB;
             float gl = 0.0f;
@@ -317,7 +336,7 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             x = x < -300.0 ? -300.0 : x;
             y = y > 300.0 ? 300.0 : y;
             y = y < -300.0 ? -300.0 : y;
-            if (k < N) out.store(k, x, y, r[j].v.x, r[j].v.y);
+            if (i < M) out.store(k, x, y, r[j].v.x, r[j].v.y);
         }
     }
     ll_sync();
@@ -341,7 +360,8 @@ __global__ __launch_bounds__(WAVE) void k_turbo_decode_lowlat(LLArgs p, const in
     for (int it = 0; it < p.iters; ++it) {
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
-        ll_siso(LLIn1{X, Le2, inv, cwl, it == 0}, LLOut1{P1, last ? Le1 : nullptr}, N, ast, bst, L, grp, sf);
+        ll_siso(LLIn1{X, Le2, inv, cwl, it == 0}, LLOut1{P1, last ? Le1 : nullptr, p.ulist, p.n_used}, N, ast, bst, L,
+                grp, sf);
         ll_siso(LLIn2{Z, P1, perm, cwl}, LLOut2{Le2}, N, ast, bst, L, grp, sf);
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]; lane l takes k = l, l + 64, ...

@@ -804,10 +804,13 @@ static int lowlat_max(const tdec_t *h) {
     }();
     return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
 }
-static bool use_lowlat(const tdec_t *h, int B) { return B <= lowlat_max(h) && B + 4 <= h->ll_cap; }
+static size_t ll_lds_bytes(int N) { return 2 * sizeof(int) * (size_t)N; }   // perm, inv_perm
+static bool use_lowlat(const tdec_t *h, int B) {
+    return B <= lowlat_max(h) && B + 4 <= h->ll_cap && ll_lds_bytes(h->N) <= 64 * 1024;
+}
 
 static int ensure_lowlat(tdec_t *h, int B) {
-    if (B > lowlat_max(h) || B + 4 <= h->ll_cap) return 0;
+    if (B > lowlat_max(h) || B + 4 <= h->ll_cap || ll_lds_bytes(h->N) > 64 * 1024) return 0;
     const int cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
     if (int rc = h->ll_ws.ensure((size_t)cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
     if (int rc = h->ll_st.ensure((size_t)cap * ll_st_elems(h->N) * sizeof(float))) return rc;
@@ -858,7 +861,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
         if (int rc = order_on(h, st)) return rc;
         LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal,
                  (const int *)h->d_ulist, h->n_used};
-        hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)B), dim3(WAVE), 0, st, a,
+        hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)B), dim3(WAVE), ll_lds_bytes(h->N), st, a,
                            (const int *)h->d_perm, (const int *)h->d_inv);
         HIPCHK(hipGetLastError());
         return mark_used(h, st);

@@ -78,16 +78,21 @@ struct LLRaw {
     double2 l;   // decoder 1: La = Le2[inv[k]]; decoder 2: P1[perm[k]] = f64(Lc) + La
 };
 
-struct LLIn1 {   // decoder 1: natural order, a-priori Le2[inv_perm[k]] (0 in the first iteration)
+// The interleaver tables are staged in LDS at the kernel's start: the alpha and
+// beta groups load different positions at the same instruction, so the index of
+// a gather is a per-lane load, and as a vector load its s_waitcnt vmcnt(0) also
+// waited for the 8-step-ahead input prefetches (every step paid the full memory
+// latency); an LDS read only waits for LDS operations.
+typedef __attribute__((address_space(3))) int lds_int;
+struct LLIn1 {   // decoder 1: natural order, a-priori Le2[inv_perm[k]] (Le2 zeroed before the first iteration)
     const float4 *X;
     const double2 *Le2;
-    const int *inv;
+    const lds_int *inv;
     int cwl;     // lane of the codeword inside its tile
-    bool first;
     __device__ __forceinline__ LLRaw load(int k) const {
         LLRaw r;
         r.v = X[(long)k * WAVE + cwl];
-        r.l = first ? make_double2(0.0, 0.0) : Le2[inv[k]];
+        r.l = Le2[inv[k]];
         return r;
     }
     __device__ __forceinline__ void gamma(const LLRaw &r, float (&g)[8], double &iA, double &iB) const {
@@ -101,7 +106,7 @@ struct LLIn1 {   // decoder 1: natural order, a-priori Le2[inv_perm[k]] (0 in th
 struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516)
     const float2 *Z;
     const double2 *P1;
-    const int *perm;
+    const lds_int *perm;
     int cwl;
     __device__ __forceinline__ LLRaw load(int k) const {
         LLRaw r;
@@ -345,6 +350,7 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
 // DVBRCS2_Turbo.decode (:464-537), one codeword per wave (block).
 __global__ __launch_bounds__(WAVE) void k_turbo_decode_lowlat(LLArgs p, const int *__restrict__ perm,
                                                               const int *__restrict__ inv) {
+    extern __shared__ int ll_lds[];   // [2][N]: perm, inv_perm
     const int lane = threadIdx.x, grp = lane >> 4;
     const long cw = blockIdx.x;
     if (cw >= p.B) return;
@@ -357,17 +363,24 @@ __global__ __launch_bounds__(WAVE) void k_turbo_decode_lowlat(LLArgs p, const in
     const float2 *Z = reinterpret_cast<const float2 *>(base + (long)N * WAVE * 4);
     double2 *P1 = p.ws + cw * ll_ws_elems(N), *Le2 = P1 + N, *Le1 = Le2 + N;
     float *ast = p.st + cw * ll_st_elems(N), *bst = ast + (N + 1) * 16;
+    lds_int *sperm = (lds_int *)ll_lds, *sinv = sperm + N;
+    for (int k = lane; k < N; k += WAVE) {
+        sperm[k] = perm[k];
+        sinv[k] = inv[k];
+        Le2[k] = make_double2(0.0, 0.0);   // the first iteration's a-priori (:490-491)
+    }
+    ll_sync();
     for (int it = 0; it < p.iters; ++it) {
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
-        ll_siso(LLIn1{X, Le2, inv, cwl, it == 0}, LLOut1{P1, last ? Le1 : nullptr, p.ulist, p.n_used}, N, ast, bst, L,
-                grp, sf);
-        ll_siso(LLIn2{Z, P1, perm, cwl}, LLOut2{Le2}, N, ast, bst, L, grp, sf);
+        ll_siso(LLIn1{X, Le2, sinv, cwl}, LLOut1{P1, last ? Le1 : nullptr, p.ulist, p.n_used}, N, ast, bst, L, grp,
+                sf);
+        ll_siso(LLIn2{Z, P1, sperm, cwl}, LLOut2{Le2}, N, ast, bst, L, grp, sf);
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]; lane l takes k = l, l + 64, ...
     for (int k = lane; k < N; k += WAVE) {
         const float4 x = X[(long)k * WAVE + cwl];
-        const double2 la = Le2[inv[k]], le = Le1[k];
+        const double2 la = Le2[sinv[k]], le = Le1[k];
         const double fa = ((double)x.x + la.x) + le.x;
         const double fb = ((double)x.y + la.y) + le.y;
         *reinterpret_cast<int2 *>(p.bits + cw * 2 * N + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);

@@ -804,7 +804,7 @@ static int lowlat_max(const tdec_t *h) {
     }();
     return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
 }
-static size_t ll_lds_bytes(int N) { return 2 * sizeof(int) * (size_t)N; }   // perm, inv_perm
+static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // perm, inv_perm, used list
 static bool use_lowlat(const tdec_t *h, int B) {
     return B <= lowlat_max(h) && B + 4 <= h->ll_cap && ll_lds_bytes(h->N) <= 64 * 1024;
 }

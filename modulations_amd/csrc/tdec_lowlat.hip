@@ -89,12 +89,14 @@ struct LLIn1 {   // decoder 1: natural order, a-priori Le2[inv_perm[k]] (Le2 zer
     const double2 *Le2;
     const lds_int *inv;
     int cwl;     // lane of the codeword inside its tile
-    __device__ __forceinline__ LLRaw load(int k) const {
+    __device__ __forceinline__ int ix(int k) const { return inv[k]; }
+    __device__ __forceinline__ LLRaw load_ix(int k, int i) const {
         LLRaw r;
         r.v = X[(long)k * WAVE + cwl];
-        r.l = Le2[inv[k]];
+        r.l = Le2[i];
         return r;
     }
+    __device__ __forceinline__ LLRaw load(int k) const { return load_ix(k, ix(k)); }
     __device__ __forceinline__ void gamma(const LLRaw &r, float (&g)[8], double &iA, double &iB) const {
         make_gamma(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
@@ -108,13 +110,15 @@ struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516
     const double2 *P1;
     const lds_int *perm;
     int cwl;
-    __device__ __forceinline__ LLRaw load(int k) const {
+    __device__ __forceinline__ int ix(int k) const { return perm[k]; }
+    __device__ __forceinline__ LLRaw load_ix(int k, int i) const {
         LLRaw r;
         const float2 z = Z[(long)k * WAVE + cwl];
         r.v = make_float4(0.0f, 0.0f, z.x, z.y);
-        r.l = P1[perm[k]];
+        r.l = P1[i];
         return r;
     }
+    __device__ __forceinline__ LLRaw load(int k) const { return load_ix(k, ix(k)); }
     __device__ __forceinline__ void gamma(const LLRaw &r, float (&g)[8], double &iA, double &iB) const {
         iA = r.l.x;
         iB = r.l.y;
@@ -134,7 +138,7 @@ struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516
 #endif
 struct LLOut1 {  // P1 = f64(Lc) + Le1 for decoder 2, Le1 itself in the last iteration
     double2 *P1, *Le1;
-    const int *ulist;
+    const lds_int *ulist;   // LDS copy (a per-lane index, as the gathers')
     int n_used;
     __device__ __forceinline__ bool sparse() const { return TDEC_LL_SKIP_UNUSED && !Le1; }
     __device__ __forceinline__ int count(int N) const { return sparse() ? n_used : N; }
@@ -219,6 +223,9 @@ template <class In> __device__ __forceinline__ void lane_pms(const In &in, const
 }
 
 constexpr int LL_D = 8;   // loads issued this many steps ahead of their use
+#ifndef TDEC_LL_PIPE
+#define TDEC_LL_PIPE 1
+#endif
 
 // One SISO (:116-281) of the wave's codeword.  ast / bst: stores [N + 1][16]
 // (lane s: element s); ast[k] = alpha2[k], bst[k] = beta2[k] on exit.
@@ -235,9 +242,56 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
         auto pos = [&](int k) { return beta ? N - 1 - k : k; };
         auto slot = [&](int k) { return (beta ? N - k : k) * 16 + s; };
         LLRaw r[LL_D];
+        float v = 0.0f;
+        if constexpr (TDEC_LL_PIPE) {
+            // Software-pipelined: the next step's pair maxima (gamma's f64 chain and
+            // two permutes) are formed while this step's neighbour permutes are in
+            // flight, and the gather indices of the group after next are read from
+            // LDS once per group, so no step waits on an index read.
+            // Every step issues the same operations (no branch around a load or a
+            // store: a merged group stores back the pass-1 value it compared
+            // against), so the compiler's wait counts stay exact.
+            int ixn[LL_D];
+            float q0, q1;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                bool merged = false;
+#pragma unroll
+                for (int j = 0; j < LL_D; ++j) r[j] = in.load(pos(min(j, N - 1)));
+#pragma unroll
+                for (int j = 0; j < LL_D; ++j) ixn[j] = in.ix(pos(min(LL_D + j, N - 1)));
+                lane_pms(in, r[0], s, R, q0, q1);
+                for (int k0 = 0; k0 < N; k0 += LL_D) {
+                    if (pass == 1 && __all(merged || grp >= 2)) break;
+                    float c[LL_D];
+#pragma unroll
+                    for (int j = 0; j < LL_D; ++j) c[j] = pass == 1 ? vst[slot(min(k0 + j, N - 1))] : 0.0f;
+                    int ixc[LL_D];
+#pragma unroll
+                    for (int j = 0; j < LL_D; ++j) {
+                        ixc[j] = ixn[j];
+                        ixn[j] = in.ix(pos(min(k0 + 2 * LL_D + j, N - 1)));
+                    }
+#pragma unroll
+                    for (int j = 0; j < LL_D; ++j) {
+                        const int k = k0 + j;
+                        if (k >= N) break;   // uniform
+                        if (pass == 1 && !merged) merged = group_all(v == c[j], L.base);
+                        const float p0 = q0, p1 = q1;
+                        const float xa = __shfl(v, R.src0), ya = __shfl(v, R.src1);
+                        lane_pms(in, r[(j + 1) % LL_D], s, R, q0, q1);   // (past N: clamped rows, unused)
+                        r[j] = in.load_ix(pos(min(k + LL_D, N - 1)), ixc[j]);
+                        const float n = fmaxf(fmaxf(NEG, xa + p0), ya + p1);
+                        const float vn = n - row_lane0(n, R.base);
+                        const bool hold = pass == 1 && merged;
+                        vst[slot(k)] = hold ? c[j] : v;
+                        v = hold ? v : vn;
+                    }
+                }
+            }
+        } else {
         float g[8], pm[8];
         double iA, iB;
-        float v = 0.0f;
         // pass 1 from 0, every vector stored
 #pragma unroll
         for (int j = 0; j < LL_D; ++j) r[j] = in.load(pos(min(j, N - 1)));
@@ -295,6 +349,7 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             }
         }
     }
+        }
     ll_sync();
     // extrinsic (:232-281) from the stored alpha2[k], beta2[k+1] at every position
     // anyone reads (out.pos(i), i < M): group q takes i = q, q + 4, ...
@@ -350,7 +405,7 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
 // DVBRCS2_Turbo.decode (:464-537), one codeword per wave (block).
 __global__ __launch_bounds__(WAVE) void k_turbo_decode_lowlat(LLArgs p, const int *__restrict__ perm,
                                                               const int *__restrict__ inv) {
-    extern __shared__ int ll_lds[];   // [2][N]: perm, inv_perm
+    extern __shared__ int ll_lds[];   // [3][N]: perm, inv_perm, the used-position list
     const int lane = threadIdx.x, grp = lane >> 4;
     const long cw = blockIdx.x;
     if (cw >= p.B) return;
@@ -363,17 +418,18 @@ __global__ __launch_bounds__(WAVE) void k_turbo_decode_lowlat(LLArgs p, const in
     const float2 *Z = reinterpret_cast<const float2 *>(base + (long)N * WAVE * 4);
     double2 *P1 = p.ws + cw * ll_ws_elems(N), *Le2 = P1 + N, *Le1 = Le2 + N;
     float *ast = p.st + cw * ll_st_elems(N), *bst = ast + (N + 1) * 16;
-    lds_int *sperm = (lds_int *)ll_lds, *sinv = sperm + N;
+    lds_int *sperm = (lds_int *)ll_lds, *sinv = sperm + N, *sused = sinv + N;
     for (int k = lane; k < N; k += WAVE) {
         sperm[k] = perm[k];
         sinv[k] = inv[k];
+        if (k < p.n_used) sused[k] = p.ulist[k];
         Le2[k] = make_double2(0.0, 0.0);   // the first iteration's a-priori (:490-491)
     }
     ll_sync();
     for (int it = 0; it < p.iters; ++it) {
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
-        ll_siso(LLIn1{X, Le2, sinv, cwl}, LLOut1{P1, last ? Le1 : nullptr, p.ulist, p.n_used}, N, ast, bst, L, grp,
+        ll_siso(LLIn1{X, Le2, sinv, cwl}, LLOut1{P1, last ? Le1 : nullptr, sused, p.n_used}, N, ast, bst, L, grp,
                 sf);
         ll_siso(LLIn2{Z, P1, sperm, cwl}, LLOut2{Le2}, N, ast, bst, L, grp, sf);
     }

@@ -800,7 +800,7 @@ placed:
 static int lowlat_max(const tdec_t *h) {
     static const int v = [] {
         const char *e = getenv("TDEC_LOWLAT_MAX");
-        return e ? std::max(0, atoi(e)) : 1024;
+        return e ? std::max(0, atoi(e)) : 4096;   // crossover: profiles/r03llmax (4096: 11.6 vs 14.5 ms, 8192: 26.1 vs 20.2)
     }();
     return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
 }

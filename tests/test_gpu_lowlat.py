@@ -1,5 +1,5 @@
 """The low-latency (state-per-lane) max-log decoder, tdec_lowlat.hip: small
-batches (B <= 1024 by default) of DVBRCS2_Turbo.decode / decode_batch /
+batches (B <= 4096 by default) of DVBRCS2_Turbo.decode / decode_batch /
 decode_device run 16 lanes per codeword.  Every case is compared bit for bit
 (hard bits and L_final, IEEE ==) with the C oracle, the restatement of
 dvb_rcs2_turbo.py:464-537 pinned to the reference's golden vectors."""

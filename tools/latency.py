@@ -19,12 +19,14 @@ def main():
     n, rate = int(sys.argv[1]) if len(sys.argv) > 1 else 752, sys.argv[2] if len(sys.argv) > 2 else "1/2"
     c = M.DVBRCS2_Turbo(n, rate)
     rng = np.random.default_rng(3)
+    batches = [int(b) for b in os.environ.get("LAT_BATCHES", "1,4,16,64,256,1024").split(",")]
+    nmax = max(batches + [1024])
     info = rng.integers(0, 2, (1024, c.k_info))
     llr = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in info[:64]])
-    llr = np.tile(llr, (16, 1))[:1024]
+    llr = np.tile(llr, (nmax // 64 + 1, 1))[:nmax]
     llr = (llr + rng.standard_normal(llr.shape) * 1.5).astype(np.float32)
     out = {"N": n, "rate": rate, "lowlat_max": os.environ.get("TDEC_LOWLAT_MAX", "default"), "batch_ms": {}}
-    for B in (1, 4, 16, 64, 256, 1024):
+    for B in batches:
         c.decode_batch(llr[:B])
         ts = []
         for _ in range(7 if B < 256 else 3):

@@ -93,3 +93,18 @@ def test_throughput_decoder_at_small_batches(n, rate):
         torch.cuda.synchronize()
         rb, rl = _oracle(c, llr)
         assert np.array_equal(bits.cpu().numpy(), rb) and np.array_equal(lf.cpu().numpy(), rl)
+
+
+@pytest.mark.parametrize("n,rate,interleaver", [(212, "1/3", "reference"), (752, "1/2", "valid-perm")])
+def test_lowlat_large_batch_matches_oracle(n, rate, interleaver):
+    """B above the 2 048 resident waves (the default crossover is 4 096): more than
+    one round of one-wave blocks; with a true permutation every position is in
+    perm's image, so decoder 1 computes every extrinsic (the used-position list
+    is the identity)."""
+    rng = np.random.default_rng(77 + n)
+    c = M.DVBRCS2_Turbo(n, rate, interleaver=interleaver)
+    B = 2500 if n == 212 else 300
+    llr = _llrs(rng, c, B, 2.0, 1.6)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    rb, rl = _oracle(c, llr)
+    assert np.array_equal(bits, rb) and np.array_equal(lf, rl)

@@ -251,8 +251,10 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
             // Every step issues the same operations (no branch around a load or a
             // store: a merged group stores back the pass-1 value it compared
             // against), so the compiler's wait counts stay exact.
+            // pair maxima two steps ahead: (c0, c1) for the next step, (n0, n1) for
+            // the one after; a step waits only for its own neighbour permutes
             int ixn[LL_D];
-            float q0, q1;
+            float c0, c1, n0, n1;
 #pragma unroll
             for (int pass = 0; pass < 2; ++pass) {
                 bool merged = false;
@@ -260,7 +262,26 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
                 for (int j = 0; j < LL_D; ++j) r[j] = in.load(pos(min(j, N - 1)));
 #pragma unroll
                 for (int j = 0; j < LL_D; ++j) ixn[j] = in.ix(pos(min(LL_D + j, N - 1)));
-                lane_pms(in, r[0], s, R, q0, q1);
+                lane_pms(in, r[0], s, R, c0, c1);
+                lane_pms(in, r[1], s, R, n0, n1);
+                // one trellis step (j: slot in the group, k: step)
+                auto step = [&](int j, int k, const float (&c)[LL_D], const int (&ixc)[LL_D]) {
+                    if (pass == 1 && !merged) merged = group_all(v == c[j], L.base);
+                    const float p0 = c0, p1 = c1;
+                    c0 = n0;
+                    c1 = n1;
+                    const float xa = __shfl(v, R.src0), ya = __shfl(v, R.src1);
+                    // the permutes go out first; the branch metrics' f64 chain below
+                    // then runs while they are in flight (the scheduler put it first)
+                    __builtin_amdgcn_sched_barrier(0);
+                    lane_pms(in, r[(j + 2) % LL_D], s, R, n0, n1);   // (past N: clamped rows, unused)
+                    r[j] = in.load_ix(pos(min(k + LL_D, N - 1)), ixc[j]);
+                    const float n = fmaxf(fmaxf(NEG, xa + p0), ya + p1);
+                    const float vn = n - row_lane0(n, R.base);
+                    const bool hold = pass == 1 && merged;
+                    vst[slot(k)] = hold ? c[j] : v;
+                    v = hold ? v : vn;
+                };
                 for (int k0 = 0; k0 < N; k0 += LL_D) {
                     if (pass == 1 && __all(merged || grp >= 2)) break;
                     float c[LL_D];
@@ -272,20 +293,15 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
                         ixc[j] = ixn[j];
                         ixn[j] = in.ix(pos(min(k0 + 2 * LL_D + j, N - 1)));
                     }
+                    if (k0 + LL_D <= N) {   // a whole group: straight-line code, no per-step branch
 #pragma unroll
-                    for (int j = 0; j < LL_D; ++j) {
-                        const int k = k0 + j;
-                        if (k >= N) break;   // uniform
-                        if (pass == 1 && !merged) merged = group_all(v == c[j], L.base);
-                        const float p0 = q0, p1 = q1;
-                        const float xa = __shfl(v, R.src0), ya = __shfl(v, R.src1);
-                        lane_pms(in, r[(j + 1) % LL_D], s, R, q0, q1);   // (past N: clamped rows, unused)
-                        r[j] = in.load_ix(pos(min(k + LL_D, N - 1)), ixc[j]);
-                        const float n = fmaxf(fmaxf(NEG, xa + p0), ya + p1);
-                        const float vn = n - row_lane0(n, R.base);
-                        const bool hold = pass == 1 && merged;
-                        vst[slot(k)] = hold ? c[j] : v;
-                        v = hold ? v : vn;
+                        for (int j = 0; j < LL_D; ++j) step(j, k0 + j, c, ixc);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < LL_D; ++j) {
+                            if (k0 + j >= N) break;   // uniform
+                            step(j, k0 + j, c, ixc);
+                        }
                     }
                 }
             }

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "tdec_api.hip")
 DEPS = [SRC, os.path.join(HERE, "csrc", "tdec_kernels.hip"), os.path.join(HERE, "csrc", "tdec_workload.hip"), os.path.join(HERE, "csrc", "npmath.hip"),
-        os.path.join(HERE, "csrc", "tdec_spl.hip"), os.path.join(HERE, "csrc", "tdec_lowlat.hip"),
+        os.path.join(HERE, "csrc", "tdec_spl.hip"), os.path.join(HERE, "csrc", "tdec_lowlat.hip"), os.path.join(HERE, "csrc", "tdec_frame.hip"),
         os.path.join(ROOT, "include", "tdec.h")]
 OUT = os.path.join(HERE, "lib", "libtdec.so")
 MODEM_SRC = os.path.join(HERE, "csrc", "modem_api.hip")

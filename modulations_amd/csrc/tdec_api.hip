@@ -18,6 +18,7 @@
 #include "tdec_workload.hip"
 #include "tdec_spl.hip"
 #include "tdec_lowlat.hip"
+#include "tdec_frame.hip"
 
 using namespace tdec;
 
@@ -805,12 +806,40 @@ static int lowlat_max(const tdec_t *h) {
     return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
 }
 static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // perm, inv_perm, used list
+// The frame decoder (tdec_frame.hip, one codeword per workgroup, everything in
+// LDS) takes the small batches when its LDS fits (N <= 790: every BASELINE
+// config); the round-3 state-per-lane decoder (tdec_lowlat.hip) otherwise, or
+// with TDEC_FRAME=0 (A/B).
+static bool frame_fits(int N, bool dec) { return fr_lds(N, dec).total <= FR_LDS_MAX; }
+static bool use_frame_decoder(const tdec_t *h) {
+    static const bool on = [] {
+        const char *e = getenv("TDEC_FRAME");
+        return !e || e[0] != '0';
+    }();
+    return on && frame_fits(h->N, true);
+}
+// One predicate for "the small-batch decoders can run on this handle" (reserve and decode).
+static bool lowlat_usable(const tdec_t *h) {
+    return lowlat_max(h) > 0 && (use_frame_decoder(h) || ll_lds_bytes(h->N) <= 64 * 1024);
+}
 static bool use_lowlat(const tdec_t *h, int B) {
-    return B <= lowlat_max(h) && B + 4 <= h->ll_cap && ll_lds_bytes(h->N) <= 64 * 1024;
+    return B <= lowlat_max(h) && B + 4 <= h->ll_cap && lowlat_usable(h);
+}
+// kernels with more than 64 KiB of dynamic LDS must say so once
+static int frame_lds_attr() {
+    static const hipError_t e = [] {
+        hipError_t r = hipFuncSetAttribute((const void *)k_turbo_decode_frame, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           FR_LDS_MAX);
+        if (r == hipSuccess)
+            r = hipFuncSetAttribute((const void *)k_siso_frame, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
+        return r;
+    }();
+    if (e != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(e));
+    return 0;
 }
 
 static int ensure_lowlat(tdec_t *h, int B) {
-    if (B > lowlat_max(h) || B + 4 <= h->ll_cap || ll_lds_bytes(h->N) > 64 * 1024) return 0;
+    if (B > lowlat_max(h) || B + 4 <= h->ll_cap || !lowlat_usable(h)) return 0;
     const int cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
     if (int rc = h->ll_ws.ensure((size_t)cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
     if (int rc = h->ll_st.ensure((size_t)cap * ll_st_elems(h->N) * sizeof(float))) return rc;
@@ -822,7 +851,7 @@ int tdec_reserve(tdec_t *h, int max_batch) {
     if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
     if (max_batch == 0) return 0;
     Guard g(h->device);
-    if (max_batch <= lowlat_max(h)) {   // small batches: the state-per-lane decoder's workspace only
+    if (max_batch <= lowlat_max(h) && lowlat_usable(h)) {   // small batches: the frame / state-per-lane decoders' workspace only
         if (max_batch + 4 > h->ll_cap || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);
         int rc = ensure_lowlat(h, max_batch);
         if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
@@ -859,6 +888,14 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     hipStream_t st = (hipStream_t)stream;
     if (use_lowlat(h, B)) {
         if (int rc = order_on(h, st)) return rc;
+        if (use_frame_decoder(h)) {
+            if (int rc = frame_lds_attr()) return rc;
+            FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used};
+            hipLaunchKernelGGL(k_turbo_decode_frame, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true).total, st, a,
+                               (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ulist);
+            HIPCHK(hipGetLastError());
+            return mark_used(h, st);
+        }
         LLArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, (float *)h->ll_st.p, d_bits, d_lfinal,
                  (const int *)h->d_ulist, h->n_used};
         hipLaunchKernelGGL(k_turbo_decode_lowlat, dim3((unsigned)B), dim3(WAVE), ll_lds_bytes(h->N), st, a,
@@ -1014,7 +1051,13 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
     const int C = (int)std::min<long>(B, chunk), waves = n_tiles_of(C);
     const size_t N = h->N, cf = (size_t)C * N * sizeof(float), cd = (size_t)C * N * sizeof(double);
-    int rc = ensure_ws(h, waves);
+    const char *se = getenv("TDEC_SISO_SPL");
+    const bool spl = se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
+    // max-log rows go to the frame SISO (one row per workgroup, tdec_frame.hip; no
+    // workspace) unless TDEC_SISO_FRAME=0 (A/B) or its LDS does not fit
+    const char *sfe = getenv("TDEC_SISO_FRAME");
+    const bool fr = !spl && h->algo == TDEC_ALGO_MAXLOG && !(sfe && sfe[0] == '0') && frame_fits(h->N, false);
+    int rc = fr ? frame_lds_attr() : ensure_ws(h, waves);
     if (!rc) rc = h->h_misc.ensure(4 * cf + 4 * cd);
     if (rc) return rc;
     char *base = (char *)h->h_misc.p;
@@ -1023,8 +1066,6 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     double *deA = (double *)(base + 4 * cf + 2 * cd), *deB = (double *)(base + 4 * cf + 3 * cd);
     hipStream_t s = h->stream;
     const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
-    const char *se = getenv("TDEC_SISO_SPL");
-    const bool spl = se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
     for (long r0 = 0; r0 < B; r0 += C) {
         const int n = (int)std::min<long>(C, B - r0), nwv = n_tiles_of(n);
         const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(float), nd = (size_t)n * N * sizeof(double);
@@ -1036,7 +1077,10 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
         HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
         SisoArgs a{n, h->N, nwv, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
         const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-        if (spl) {   // A/B prototype: one state per lane, 4 codewords per wave (tdec_spl.hip)
+        if (fr) {
+            FrSisoArgs fa{n, h->N, dA, dB, dW, dY, daA, daB, sf, deA, deB};
+            hipLaunchKernelGGL(k_siso_frame, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
+        } else if (spl) {   // A/B prototype: one state per lane, 4 codewords per wave (tdec_spl.hip)
             const long sw = (n + 3) / 4;                     // waves
             const long stride = ((h->N + SPL_W - 1) / SPL_W + RING) * 64L;
             if (int rc = h->spl_ck.ensure(sizeof(float) * stride * ((sw + 3) / 4 * 4))) return rc;

@@ -1,0 +1,477 @@
+// tdec_frame.hip -- the FRAME decoder (max-log): ONE CODEWORD PER WORKGROUP.
+//
+// The per-call paths of the reference -- DVBRCS2_Turbo.decode() once per frame
+// (test.py:81) and bcjr_max_log_map() once per call (dvb_rcs2_turbo.py:116-281)
+// -- are latency problems: one codeword, 16 (or 1) SISOs, each a chain of
+// ~2N dependent trellis steps.  Here a 512-thread workgroup owns the codeword
+// and everything lives in LDS (alpha / beta stores, the pair-maxima table, the
+// extrinsic planes, the interleaver tables).  One SISO is three phases,
+// separated by workgroup barriers:
+//
+//  P  branch metrics, position-parallel (every thread one position): the
+//     reference's f64 gamma (:127-160), rounded to f32, reduced to the 8 pair
+//     maxima a recursion step reads, into an LDS table.
+//  R  the recursions: wave 0 runs alpha, wave 1 beta (:162-230), each on 4
+//     16-lane groups, one trellis state per lane.
+//       * No cross-lane permute on the chain.  State ns has predecessors
+//         rotr(ns) and rotr(ns)^8 (4-bit rotations: ns = ((s<<1)&14)|dk), so
+//         with a TIME-VARYING labelling -- lane l holds state rotl^t(l) at step
+//         t (beta: rotr^t(rev(l))) -- one predecessor is the lane itself and
+//         the other is lane l ^ (8 >> (t % 4)): a DPP move (row_ror:8, two
+//         bank-masked row shifts, quad_perm).  The state-0 normalisation reads
+//         lane 0 of the row (row_newbcast:0; state 0 is always lane 0).  A step
+//         is DPP, two adds, max3, DPP, subtract: no LDS round trip.
+//       * Segments, exact.  The 4 groups of a wave take 4 segments of the
+//         block.  Segment 0 starts from the reference's zero vector; the others
+//         start from zero as a guess, then re-run from their predecessor's true
+//         end vector until their vector EQUALS the stored one (IEEE ==): from
+//         there the stored trajectory is the same deterministic f32 map of the
+//         same vector, so it is the reference's (the merge argument of
+//         DESIGN §3 item 2).  A segment that reaches its end without merging
+//         hands its new end vector to the next one (rounds until none changes:
+//         at most 4).  The reference's second pass (from alpha1[N] / beta1[0])
+//         is the same machinery started at segment 0.  Every stored vector is
+//         therefore the reference's alpha2 / beta2, bit for bit.
+//  E  the extrinsic (:232-281), position-parallel, from the stored alpha2[k],
+//     beta2[k+1] and the recomputed branch metrics (extrinsic<0>, the per-lane
+//     decoder's code).
+// Same f32 / f64 operations as the reference everywhere; maxima are order-free
+// (fmaxf drops a NaN as the strict `>` does; only the sign of an exact zero can
+// differ, compared with IEEE ==).  tests/test_gpu_frame.py.
+namespace tdec {
+
+constexpr int FR_WAVES = 8;
+constexpr int FR_BLOCK = FR_WAVES * WAVE;
+typedef __attribute__((address_space(3))) char lds_b;   // byte-addressed LDS
+
+__device__ __forceinline__ float lds_ld(const lds_b *p) { return *(const lds_f1 *)p; }
+__device__ __forceinline__ void lds_st(lds_b *p, float v) { *(lds_f1 *)p = v; }
+
+// ---- LDS layout (bytes) ------------------------------------------------------------
+// ev [2][4][16] f32 segment end vectors, sink [2][512 B] (stores of idle groups),
+// st_a [N+1][16] f32 (alpha[k] at row k), st_b [N+1][16] (beta[k] at row k), pmt
+// [N][8] f32 pair maxima; the decoder adds p1, le2 [N] double2 and perm, inv,
+// ulist [N] int.  The recursions read up to 8 rows past pmt / st in either
+// direction (prefetch; values unused): the arrays before st_a and the tail pad
+// keep those reads inside the allocation.
+struct FrLds {
+    int st_a, st_b, pmt, ev, sink, p1, le2, perm, inv, ulist, total;
+};
+__host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
+    FrLds L{};
+    int o = 0;
+    L.ev = o;   o += 2 * 4 * 64;
+    L.sink = o; o += 2 * 512;
+    L.st_a = o; o += (N + 1) * 64;
+    L.st_b = o; o += (N + 1) * 64;
+    L.pmt = o;  o += N * 32;
+    L.p1 = L.le2 = L.perm = L.inv = L.ulist = o;
+    if (dec) {
+        L.p1 = o;    o += N * 16;
+        L.le2 = o;   o += N * 16;
+        L.perm = o;  o += N * 4;
+        L.inv = o;   o += N * 4;
+        L.ulist = o; o += N * 4;
+    }
+    L.total = o + 512;   // tail: the alpha wave's reads past pmt
+    return L;
+}
+constexpr int FR_LDS_MAX = 160 * 1024;
+
+// ---- lane labelling ------------------------------------------------------------------
+__host__ __device__ constexpr int rotl4(int x, int r) {
+    r &= 3;
+    return ((x << r) | (x >> (4 - r))) & 15;
+}
+__host__ __device__ constexpr int rotr4(int x, int r) { return rotl4(x, 4 - (r & 3)); }
+__host__ __device__ constexpr int rev4(int x) { return ((x & 1) << 3) | ((x & 2) << 1) | ((x & 4) >> 1) | ((x & 8) >> 3); }
+// pair-maxima index (pair_max: class A^B * 4 + 2W + Y) of the branch pair p -> ns
+__host__ __device__ constexpr int pair_ix(int p, int ns) {
+    for (int inp = 0; inp < 4; ++inp)
+        if (t_next(p, inp) == ns) return ((((inp >> 1) ^ inp) & 1) << 2) | (t_ow(p, inp) << 1) | t_oy(p, inp);
+    return 0;
+}
+
+// Per-lane constants of a recursion lane, for the 4 phases ph = t % 4 of a step.
+// lbl[ph]: state of the lane's element of the vector entering a phase-ph step
+// (alpha: rotl^ph(l); beta: rotr^ph(rev(l))); soff: its byte offset in a store row
+// plus the row step from the block's first row; poff: the pm-table offsets of
+// the lane's own pair and its partner's (lane l ^ (8 >> ph)) pair, likewise.
+template <int DIR> struct FrLane {
+    int lbl[4];
+    int soff[4];
+    int poff[4][2];
+};
+template <int DIR> __device__ __forceinline__ FrLane<DIR> fr_lane(int l) {
+    FrLane<DIR> L;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+        int in, a, b;
+        if (DIR == 0) {   // alpha: produces ns = rotl^(ph+1)(l) from in = rotr(ns) (self) and in ^ 8 (partner)
+            in = rotl4(l, ph);
+            const int ns = rotl4(l, ph + 1);
+            a = pair_ix(in, ns);
+            b = pair_ix(in ^ 8, ns);
+        } else {          // beta: produces s = rotr^(ph+1)(rev l) from its successors in = rotl(s) and in ^ 1
+            in = rotr4(rev4(l), ph);
+            const int s = rotr4(rev4(l), ph + 1);
+            a = pair_ix(s, in);
+            b = pair_ix(s, in ^ 1);
+        }
+        const int dir = DIR ? -1 : 1;
+        L.lbl[ph] = in;
+        L.soff[ph] = dir * 64 * ph + 4 * in;
+        L.poff[ph][0] = dir * 32 * ph + 4 * a;
+        L.poff[ph][1] = dir * 32 * ph + 4 * b;
+    }
+    return L;
+}
+
+// v of lane l ^ (8 >> PH) within the 16-lane row
+template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
+    const int i = __float_as_int(v);
+    if constexpr (PH == 0) return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x128, 0xF, 0xF, false));   // row_ror:8
+    if constexpr (PH == 1) {   // lanes of banks 0, 2 read l + 4 (row_shl:4), banks 1, 3 read l - 4 (row_shr:4)
+        const int t = __builtin_amdgcn_mov_dpp(i, 0x104, 0xF, 0x5, false);
+        return __int_as_float(__builtin_amdgcn_update_dpp(t, i, 0x114, 0xF, 0xA, false));
+    }
+    if constexpr (PH == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+    return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false));                           // quad_perm [1,0,3,2]
+}
+// one trellis step (:165-179 / :203-213 with pair maxima): max over the two branch
+// pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row)
+template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po) {
+    const float o = fr_xchg<PH>(v);
+    const float n = fmaxf(fmaxf(NEG, v + ps), o + po);
+    return n - __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));   // row_newbcast:0
+}
+
+// lanes of the 16-lane groups whose 16 bits of m are all set
+__device__ __forceinline__ unsigned long long grp_all16(unsigned long long m) {
+    unsigned long long r = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+        if (((m >> (16 * g)) & 0xFFFFull) == 0xFFFFull) r |= 0xFFFFull << (16 * g);
+    return r;
+}
+
+struct FrRec {
+    lds_b *st;     // this direction's store
+    lds_b *pmt;    // pair maxima [N][8]
+    lds_b *ev;     // [4][16] end vectors of this direction
+    lds_b *sink;   // 512 B
+    int N;
+};
+
+#ifndef TDEC_FR_STATS
+#define TDEC_FR_STATS 0
+#endif
+#if TDEC_FR_STATS
+__device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, pass 2; rounds: fix-up, pass 2; SISOs
+#endif
+
+// One round of the groups in `run` (wave-uniform lane mask), each from its start
+// vector v over its segment [u0, u0 + len) of the direction's step order:
+// stores every vector entering a step; with CMP, stops a group at the first
+// block start where its vector equals the stored one (merged).  Returns the
+// lanes of the groups that reached their segment's end (their end vector, the
+// one entering step u0 + len, is in ev[g]).
+template <int DIR, bool CMP>
+__device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrLane<DIR> &L, int g, int lane, int u0,
+                                                       int len, unsigned long long run, float v) {
+    const int N = R.N;
+    // byte offsets of the rows of step U: store row (alpha[U] / beta[N - U]) and pm row (position)
+    auto srow = [&](int U) { return (DIR ? N - U : U) * 64; };
+    auto prow = [&](int U) { return (DIR ? N - 1 - U : U) * 32; };
+    lds_b *const sink_s = R.sink + (DIR ? 256 : 0);
+    unsigned long long reached = 0;
+    float pc[4][2], pn[4][2];
+    float cmpv = 0.0f, cmpn = 0.0f;
+    {
+        const lds_b *pr = R.pmt + prow(u0);
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            pc[ph][0] = lds_ld(pr + L.poff[ph][0]);
+            pc[ph][1] = lds_ld(pr + L.poff[ph][1]);
+        }
+        if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
+    }
+    for (int u = 0;; u += 4) {
+#if TDEC_FR_STATS
+        if (lane == 0 && run) atomicAdd(&g_fr_stats[CMP ? (u0 == 0 && (run & 1) ? 2 : 1) : 0], 1ull);
+#endif
+        if constexpr (CMP) run &= ~grp_all16(__ballot(v == cmpv));   // merged: the rest is stored already
+        if (!run) break;
+        const int U = u0 + u;
+        // the next block's pair maxima and compare value (rows past the end are read, unused)
+        {
+            const lds_b *pr = R.pmt + prow(U + 4);
+#pragma unroll
+            for (int ph = 0; ph < 4; ++ph) {
+                pn[ph][0] = lds_ld(pr + L.poff[ph][0]);
+                pn[ph][1] = lds_ld(pr + L.poff[ph][1]);
+            }
+            if constexpr (CMP) cmpn = lds_ld(R.st + srow(U + 4) + L.soff[0]);
+        }
+        const bool rl = (run >> lane) & 1;
+        lds_b *const srw = R.st + srow(U);
+        if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
+            lds_b *const sr = rl ? srw : sink_s;
+            lds_st(sr + L.soff[0], v);
+            v = fr_step<0>(v, pc[0][0], pc[0][1]);
+            lds_st(sr + L.soff[1], v);
+            v = fr_step<1>(v, pc[1][0], pc[1][1]);
+            lds_st(sr + L.soff[2], v);
+            v = fr_step<2>(v, pc[2][0], pc[2][1]);
+            lds_st(sr + L.soff[3], v);
+            v = fr_step<3>(v, pc[3][0], pc[3][1]);
+        } else {   // some group ends in this block: per-step bounds, end vector captured
+            lds_b *const evg = R.ev + g * 64;
+#define FR_SLOW_STEP(PH)                                                       \
+    {                                                                          \
+        const int uu = u + PH;                                                 \
+        if (rl && uu < len) lds_st(srw + L.soff[PH], v);                       \
+        const float vn = fr_step<PH>(v, pc[PH][0], pc[PH][1]);                 \
+        if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(PH + 1) & 3], vn);    \
+        v = vn;                                                                \
+    }
+            FR_SLOW_STEP(0) FR_SLOW_STEP(1) FR_SLOW_STEP(2) FR_SLOW_STEP(3)
+#undef FR_SLOW_STEP
+            const unsigned long long ended = __ballot(u + 4 >= len) & run;
+            reached |= ended;
+            run &= ~ended;
+        }
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            pc[ph][0] = pn[ph][0];
+            pc[ph][1] = pn[ph][1];
+        }
+        cmpv = cmpn;
+    }
+    return reached;
+}
+
+// Both passes of one direction (alpha: :162-197, beta: :199-230) by one wave.
+// On exit row k of R.st holds alpha2[k] (k < N) / beta2[k] (k >= 1).
+template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
+    const int l = lane & 15, g = lane >> 4;
+    const FrLane<DIR> L = fr_lane<DIR>(l);
+    const int N = R.N;
+    const int Ls = (N + 15) / 16 * 4;       // segment length (a multiple of 4)
+    const int nseg = (N + Ls - 1) / Ls;     // 1..4
+    const int len = max(0, min(Ls, N - g * Ls)), u0 = len ? g * Ls : 0;   // empty segments never run
+    const unsigned long long all = nseg == 4 ? ~0ull : (1ull << (16 * nseg)) - 1;
+    const lds_b *src = R.ev + (g == 0 ? nseg - 1 : g - 1) * 64 + 4 * L.lbl[0];   // the start of a re-run
+    // pass 1: every segment from zero (segment 0: the reference's start), then the
+    // re-runs from each predecessor's end until nothing changes
+    unsigned long long reached = fr_round<DIR, false>(R, L, g, lane, u0, len, all, 0.0f);
+    unsigned long long dirty = (reached << 16) & all;
+    while (dirty) {
+#if TDEC_FR_STATS
+        if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
+#endif
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src));
+        dirty = (reached << 16) & all;
+    }
+    // pass 2 from the pass-1 end vector (alpha1[N] / beta1[0]) at segment 0
+    dirty = 0xFFFFull;
+    do {
+#if TDEC_FR_STATS
+        if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
+#endif
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src));
+        dirty = (reached << 16) & all;
+    } while (dirty);
+}
+
+// ---- inputs / outputs of one SISO -------------------------------------------------------
+// get(k): the f64 sums inA = f64(Lc_A) + La_A, inB (:135-136), the parities and Lc.
+struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[k]] (LDS)
+    const float4 *X;
+    const lds_b *le2;
+    const lds_int *inv;
+    int cwl;
+    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
+        const float4 x = X[(long)k * WAVE + cwl];
+        const d2v p = *(const lds_d2 *)(le2 + 16 * inv[k]);
+        iA = (double)x.x + p.x;
+        iB = (double)x.y + p.y;
+        w = x.z;
+        y = x.w;
+        la = x.x;
+        lb = x.y;
+    }
+};
+struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 (LDS; :507-516)
+    const float2 *Z;
+    const lds_b *p1;
+    const lds_int *perm;
+    int cwl;
+    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
+        const float2 z = Z[(long)k * WAVE + cwl];
+        const d2v p = *(const lds_d2 *)(p1 + 16 * perm[k]);
+        iA = p.x;
+        iB = p.y;
+        w = z.x;
+        y = z.y;
+        la = lb = 0.0f;
+    }
+};
+struct FrInRow {   // bcjr_max_log_map's arguments (:116), one row
+    const float *A, *B, *W, *Y;
+    const double *LaA, *LaB;
+    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
+        iA = (double)A[k] + LaA[k];
+        iB = (double)B[k] + LaB[k];
+        w = W[k];
+        y = Y[k];
+        la = lb = 0.0f;
+    }
+};
+struct FrOut1 {  // P1 = f64(Lc) + Le1 for decoder 2 (LDS), Le1 itself in the last iteration (global)
+    lds_b *p1;
+    double2 *le1;
+    const lds_int *ulist;   // the positions in perm's image (only those are read before the last iteration)
+    int n_used;
+    __device__ __forceinline__ bool sparse() const { return !le1; }
+    __device__ __forceinline__ int count(int N) const { return sparse() ? n_used : N; }
+    __device__ __forceinline__ int pos(int i) const {
+        return sparse() ? ulist[i] : i;
+    }
+    __device__ __forceinline__ void store(int k, double a, double b, float la, float lb) const {
+        *(lds_d2 *)(p1 + 16 * k) = d2v{(double)la + a, (double)lb + b};
+        if (le1) le1[k] = make_double2(a, b);
+    }
+};
+struct FrOut2 {
+    lds_b *le2;
+    __device__ __forceinline__ int count(int N) const { return N; }
+    __device__ __forceinline__ int pos(int i) const { return i; }
+    __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
+        *(lds_d2 *)(le2 + 16 * k) = d2v{a, b};
+    }
+};
+struct FrOutRow {
+    double *A, *B;
+    __device__ __forceinline__ int count(int N) const { return N; }
+    __device__ __forceinline__ int pos(int i) const { return i; }
+    __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
+        A[k] = a;
+        B[k] = b;
+    }
+};
+
+// One SISO (:116-281) of the workgroup's codeword.  Ends with a barrier.
+template <class In, class Out>
+__device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo, int N, double sf) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    lds_b *pmt = sm + Lo.pmt;
+    // P: pair maxima of every position
+    for (int k = tid; k < N; k += FR_BLOCK) {
+        double iA, iB;
+        float w, y, la, lb;
+        in.get(k, iA, iB, w, y, la, lb);
+        float g[8], pm[2][4];
+        gamma_from_sums(iA, iB, w, y, g);
+        pair_max(g, pm);
+        lds_f4 *d = (lds_f4 *)(pmt + 32 * k);
+        d[0] = f4v{pm[0][0], pm[0][1], pm[0][2], pm[0][3]};
+        d[1] = f4v{pm[1][0], pm[1][1], pm[1][2], pm[1][3]};
+    }
+    __syncthreads();
+    // R: alpha on wave 0, beta on wave 1
+    if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
+    else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + 256, sm + Lo.sink + 512, N}, lane);
+    __syncthreads();
+    // E: extrinsic of every position anyone reads
+    const int M = out.count(N);
+    for (int i = tid; i < M; i += FR_BLOCK) {
+        const int k = out.pos(i);
+        double iA, iB;
+        float w, y, la, lb;
+        in.get(k, iA, iB, w, y, la, lb);
+        float g[8];
+        gamma_from_sums(iA, iB, w, y, g);
+        float a[NS], b[NS];
+        const lds_f4 *ra = (const lds_f4 *)(sm + Lo.st_a + 64 * k), *rb = (const lds_f4 *)(sm + Lo.st_b + 64 * (k + 1));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f4v x = ra[q], z = rb[q];
+            a[4 * q] = x.x, a[4 * q + 1] = x.y, a[4 * q + 2] = x.z, a[4 * q + 3] = x.w;
+            b[4 * q] = z.x, b[4 * q + 1] = z.y, b[4 * q + 2] = z.z, b[4 * q + 3] = z.w;
+        }
+        double leA, leB;
+        extrinsic<0>(a, g, b, iA, iB, sf, leA, leB);
+        out.store(k, leA, leB, la, lb);
+    }
+    __syncthreads();
+}
+
+struct FrArgs {
+    int B, N, iters;
+    const float *planes;   // tile layout of k_depuncture / k_demap_planes
+    double2 *le1;          // [B][N]: the last iteration's Le1 (global scratch)
+    int32_t *bits;         // [B][2N]
+    double *lfinal;        // [B][2N] or null
+    int n_used;
+};
+
+// DVBRCS2_Turbo.decode (:464-537) of one codeword per workgroup (grid = B).
+__global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
+                                                                 const int *__restrict__ inv,
+                                                                 const int *__restrict__ ulist) {
+    extern __shared__ float4 fr_sm[];
+    lds_b *sm = (lds_b *)fr_sm;
+    const int N = p.N, tid = threadIdx.x;
+    const long cw = blockIdx.x;
+    const FrLds Lo = fr_lds(N, true);
+    const long tile = cw / WAVE;
+    const int cwl = (int)(cw % WAVE);
+    const float *base = p.planes + tile * tile_floats(N);
+    const float4 *X = reinterpret_cast<const float4 *>(base);
+    const float2 *Z = reinterpret_cast<const float2 *>(base + (long)N * WAVE * 4);
+    lds_int *sperm = (lds_int *)(sm + Lo.perm), *sinv = (lds_int *)(sm + Lo.inv), *sul = (lds_int *)(sm + Lo.ulist);
+    for (int k = tid; k < N; k += FR_BLOCK) {
+        sperm[k] = perm[k];
+        sinv[k] = inv[k];
+        if (k < p.n_used) sul[k] = ulist[k];
+        *(lds_d2 *)(sm + Lo.le2 + 16 * k) = d2v{0.0, 0.0};   // the first iteration's a-priori (:490-491)
+    }
+    __syncthreads();
+    double2 *le1 = p.le1 + cw * N;
+    for (int it = 0; it < p.iters; ++it) {
+        const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
+        const bool last = it == p.iters - 1;
+        fr_siso(FrIn1{X, sm + Lo.le2, sinv, cwl}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, sul, p.n_used}, sm, Lo, N,
+                sf);
+        fr_siso(FrIn2{Z, sm + Lo.p1, sperm, cwl}, FrOut2{sm + Lo.le2}, sm, Lo, N, sf);
+    }
+    // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
+    for (int k = tid; k < N; k += FR_BLOCK) {
+        const float4 x = X[(long)k * WAVE + cwl];
+        const d2v la = *(const lds_d2 *)(sm + Lo.le2 + 16 * sinv[k]);
+        const double2 le = le1[k];
+        const double fa = ((double)x.x + la.x) + le.x;
+        const double fb = ((double)x.y + la.y) + le.y;
+        *reinterpret_cast<int2 *>(p.bits + cw * 2 * N + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
+        if (p.lfinal) *reinterpret_cast<double2 *>(p.lfinal + cw * 2 * N + 2 * k) = make_double2(fa, fb);
+    }
+}
+
+// bcjr_max_log_map (:116-281) on [B][N] rows, one row per workgroup.
+struct FrSisoArgs {
+    int B, N;
+    const float *LcA, *LcB, *LcW, *LcY;
+    const double *LaA, *LaB;
+    double sf;
+    double *LeA, *LeB;
+};
+__global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
+    extern __shared__ float4 fr_sm[];
+    lds_b *sm = (lds_b *)fr_sm;
+    const long row = (long)blockIdx.x * p.N;
+    fr_siso(FrInRow{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row},
+            FrOutRow{p.LeA + row, p.LeB + row}, sm, fr_lds(p.N, false), p.N, p.sf);
+}
+
+}  // namespace tdec

@@ -812,11 +812,8 @@ static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // p
 // with TDEC_FRAME=0 (A/B).
 static bool frame_fits(int N, bool dec) { return fr_lds(N, dec).total <= FR_LDS_MAX; }
 static bool use_frame_decoder(const tdec_t *h) {
-    static const bool on = [] {
-        const char *e = getenv("TDEC_FRAME");
-        return !e || e[0] != '0';
-    }();
-    return on && frame_fits(h->N, true);
+    const char *e = getenv("TDEC_FRAME");   // read per call: tests switch decoders in-process
+    return !(e && e[0] == '0') && frame_fits(h->N, true);
 }
 // One predicate for "the small-batch decoders can run on this handle" (reserve and decode).
 static bool lowlat_usable(const tdec_t *h) {
@@ -1037,6 +1034,19 @@ int tdec_host_alloc(size_t bytes, void **out) {
 void tdec_host_free(void *p) {
     if (p) hipHostFree(p);
 }
+
+#if TDEC_FR_STATS
+// measurement build only: the frame decoder's block / round counters since the last
+// call (blocks of 4 steps: phase A, fix-up rounds, pass 2; rounds: fix-up, pass 2)
+int tdec_frame_stats(unsigned long long *out) {
+    hipDeviceSynchronize();
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fr_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(TDEC_EHIP, "g_fr_stats");
+    const unsigned long long z[8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_fr_stats), z, sizeof(z));
+    return 0;
+}
+#endif
 
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
                     const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {

@@ -167,7 +167,7 @@ struct FrRec {
 #define TDEC_FR_STATS 0
 #endif
 #if TDEC_FR_STATS
-__device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, pass 2; rounds: fix-up, pass 2; SISOs
+__device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, pass 2; rounds: fix-up, pass 2
 #endif
 
 // One round of the groups in `run` (wave-uniform lane mask), each from its start
@@ -178,14 +178,14 @@ __device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, p
 // one entering step u0 + len, is in ev[g]).
 template <int DIR, bool CMP>
 __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrLane<DIR> &L, int g, int lane, int u0,
-                                                       int len, unsigned long long run, float v) {
+                                                       int len, unsigned long long run, float v, int stat) {
     const int N = R.N;
     // byte offsets of the rows of step U: store row (alpha[U] / beta[N - U]) and pm row (position)
     auto srow = [&](int U) { return (DIR ? N - U : U) * 64; };
     auto prow = [&](int U) { return (DIR ? N - 1 - U : U) * 32; };
     lds_b *const sink_s = R.sink + (DIR ? 256 : 0);
     unsigned long long reached = 0;
-    float pc[4][2], pn[4][2];
+    float pc[4][2], pn[4][2] = {};
     float cmpv = 0.0f, cmpn = 0.0f;
     {
         const lds_b *pr = R.pmt + prow(u0);
@@ -196,42 +196,44 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         }
         if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
     }
-    for (int u = 0;; u += 4) {
+    // one block of 4 steps from pair maxima `c` while the next block's go to `n`
+    // (ping-pong over two register sets: no moves between blocks)
+    auto block = [&](int u, float (&c)[4][2], float (&n)[4][2], float &cv, float &cn) -> bool {
 #if TDEC_FR_STATS
-        if (lane == 0 && run) atomicAdd(&g_fr_stats[CMP ? (u0 == 0 && (run & 1) ? 2 : 1) : 0], 1ull);
+        if (lane == 0) atomicAdd(&g_fr_stats[stat], 1ull);
 #endif
-        if constexpr (CMP) run &= ~grp_all16(__ballot(v == cmpv));   // merged: the rest is stored already
-        if (!run) break;
+        if constexpr (CMP) run &= ~grp_all16(__ballot(v == cv));   // merged: the rest is stored already
+        if (!run) return false;
         const int U = u0 + u;
         // the next block's pair maxima and compare value (rows past the end are read, unused)
         {
             const lds_b *pr = R.pmt + prow(U + 4);
 #pragma unroll
             for (int ph = 0; ph < 4; ++ph) {
-                pn[ph][0] = lds_ld(pr + L.poff[ph][0]);
-                pn[ph][1] = lds_ld(pr + L.poff[ph][1]);
+                n[ph][0] = lds_ld(pr + L.poff[ph][0]);
+                n[ph][1] = lds_ld(pr + L.poff[ph][1]);
             }
-            if constexpr (CMP) cmpn = lds_ld(R.st + srow(U + 4) + L.soff[0]);
+            if constexpr (CMP) cn = lds_ld(R.st + srow(U + 4) + L.soff[0]);
         }
         const bool rl = (run >> lane) & 1;
         lds_b *const srw = R.st + srow(U);
         if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
             lds_b *const sr = rl ? srw : sink_s;
             lds_st(sr + L.soff[0], v);
-            v = fr_step<0>(v, pc[0][0], pc[0][1]);
+            v = fr_step<0>(v, c[0][0], c[0][1]);
             lds_st(sr + L.soff[1], v);
-            v = fr_step<1>(v, pc[1][0], pc[1][1]);
+            v = fr_step<1>(v, c[1][0], c[1][1]);
             lds_st(sr + L.soff[2], v);
-            v = fr_step<2>(v, pc[2][0], pc[2][1]);
+            v = fr_step<2>(v, c[2][0], c[2][1]);
             lds_st(sr + L.soff[3], v);
-            v = fr_step<3>(v, pc[3][0], pc[3][1]);
+            v = fr_step<3>(v, c[3][0], c[3][1]);
         } else {   // some group ends in this block: per-step bounds, end vector captured
             lds_b *const evg = R.ev + g * 64;
 #define FR_SLOW_STEP(PH)                                                       \
     {                                                                          \
         const int uu = u + PH;                                                 \
         if (rl && uu < len) lds_st(srw + L.soff[PH], v);                       \
-        const float vn = fr_step<PH>(v, pc[PH][0], pc[PH][1]);                 \
+        const float vn = fr_step<PH>(v, c[PH][0], c[PH][1]);                   \
         if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(PH + 1) & 3], vn);    \
         v = vn;                                                                \
     }
@@ -241,12 +243,11 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
             reached |= ended;
             run &= ~ended;
         }
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-            pc[ph][0] = pn[ph][0];
-            pc[ph][1] = pn[ph][1];
-        }
-        cmpv = cmpn;
+        return true;
+    };
+    for (int u = 0;; u += 8) {
+        if (!block(u, pc, pn, cmpv, cmpn)) break;
+        if (!block(u + 4, pn, pc, cmpn, cmpv)) break;
     }
     return reached;
 }
@@ -264,13 +265,13 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     const lds_b *src = R.ev + (g == 0 ? nseg - 1 : g - 1) * 64 + 4 * L.lbl[0];   // the start of a re-run
     // pass 1: every segment from zero (segment 0: the reference's start), then the
     // re-runs from each predecessor's end until nothing changes
-    unsigned long long reached = fr_round<DIR, false>(R, L, g, lane, u0, len, all, 0.0f);
+    unsigned long long reached = fr_round<DIR, false>(R, L, g, lane, u0, len, all, 0.0f, 0);
     unsigned long long dirty = (reached << 16) & all;
     while (dirty) {
 #if TDEC_FR_STATS
         if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src));
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
         dirty = (reached << 16) & all;
     }
     // pass 2 from the pass-1 end vector (alpha1[N] / beta1[0]) at segment 0
@@ -279,7 +280,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 #if TDEC_FR_STATS
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src));
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 2);
         dirty = (reached << 16) & all;
     } while (dirty);
 }

@@ -244,6 +244,108 @@ def gen_decode(T):
     np.savez_compressed(os.path.join(OUT, "decode.npz"), **out)
 
 
+def gen_nonfinite(T):
+    """Non-finite inputs through the reference: SISO calls and
+    full decodes whose LLRs / a-priori values hold NaN, +inf, -inf (scattered,
+    whole rows, mixed), and the harness chain compute_llr -> decode with NaN and
+    inf symbols (test_sdr_with_coding.py:213-225: a NaN symbol gives NaN LLRs).
+    The reference's strict `>` recursions (:174-176, :247-248) drop NaN
+    candidates and its `if` clip (:276-279) passes NaN through; these vectors
+    pin what that does end to end."""
+    rng = np.random.default_rng(2024)
+    c = make_codec(T, 48, "1/3")
+    tabs = (c.next_state, c.out_W, c.out_Y, c.prev_state, c.prev_input)
+    out = {}
+    kinds = ("nan", "pinf", "ninf", "mixed", "row_nan", "la_nan", "la_inf", "inf_both")
+    for n in (48, 212, 752):
+        LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB = ([] for _ in range(8))
+        for kind in kinds:
+            Lc = (rng.standard_normal((4, n)) * 3.0).astype(np.float32)
+            La = rng.standard_normal((2, n)) * 6.0
+            pos = rng.integers(0, n, max(2, n // 16))
+            if kind == "nan":
+                Lc[rng.integers(0, 4), pos] = np.nan
+            elif kind == "pinf":
+                Lc[rng.integers(0, 4), pos] = np.inf
+            elif kind == "ninf":
+                Lc[rng.integers(0, 4), pos] = -np.inf
+            elif kind == "mixed":
+                Lc[0, pos[0::3]] = np.nan
+                Lc[2, pos[1::3]] = np.inf
+                Lc[3, pos[2::3]] = -np.inf
+            elif kind == "row_nan":
+                Lc[1, :] = np.nan
+            elif kind == "la_nan":
+                La[0, pos] = np.nan
+            elif kind == "la_inf":
+                La[1, pos] = np.inf
+                La[0, pos[::2]] = -np.inf
+            elif kind == "inf_both":
+                Lc[0, pos] = np.inf
+                Lc[1, pos] = -np.inf
+            a, b = T.bcjr_max_log_map(Lc[0], Lc[1], Lc[2], Lc[3], La[0], La[1], *tabs, n, 0.7)
+            for lst, v in zip((LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB), (*Lc, *La, a, b)):
+                lst.append(v)
+        out.update({f"siso_{k}_{n}": np.stack(v) for k, v in
+                    zip(("LcA", "LcB", "LcW", "LcY", "LaA", "LaB", "LeA", "LeB"),
+                        (LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB))})
+    out["siso_kinds"] = np.array(kinds)
+    # full decodes (stable inverse interleaver, as the decode.npz 'stable' vectors)
+    for n, rate in ((48, "1/3"), (212, "1/3"), (752, "1/2")):
+        cc = make_codec(T, n, rate)
+        cc.inv_perm = np.argsort(cc.perm, kind="stable").astype(np.int32)
+        key = f"{n}_{rate.replace('/', '_')}"
+        llrs, bits, lfs = [], [], []
+        for kind in ("nan", "pinf", "ninf", "mixed", "row_nan"):
+            info = rng.integers(0, 2, cc.k_info)
+            llr = ((1 - 2.0 * cc.encode(info)) * 2.0 + rng.standard_normal(cc.n_coded) * 1.2).astype(np.float32)
+            pos = rng.integers(0, cc.n_coded, max(3, cc.n_coded // 40))
+            if kind == "nan":
+                llr[pos] = np.nan
+            elif kind == "pinf":
+                llr[pos] = np.inf
+            elif kind == "ninf":
+                llr[pos] = -np.inf
+            elif kind == "mixed":
+                llr[pos[0::3]] = np.nan
+                llr[pos[1::3]] = np.inf
+                llr[pos[2::3]] = -np.inf
+            else:
+                llr[:] = np.nan
+            t = time.time()
+            b, lf = _decode_capture(T, cc, llr)
+            print(f"  nonfinite decode {key} {kind} ({time.time() - t:.1f}s)", flush=True)
+            llrs.append(llr); bits.append(b); lfs.append(lf)
+        out[f"dec_llr_{key}"] = np.stack(llrs)
+        out[f"dec_bits_{key}"] = np.stack(bits)
+        out[f"dec_lfinal_{key}"] = np.stack(lfs)
+        out[f"dec_inv_{key}"] = cc.inv_perm
+    # the harness chain: 16QAM symbols with NaN / inf entries -> compute_llr
+    # (test_sdr_with_coding.py:200-225) -> the decoder's sign -> decode (N=212, r=1/3)
+    import types
+    T.DVB_RCS2_TurboCodec = None
+    sys.modules.setdefault("matplotlib", types.ModuleType("matplotlib"))
+    mpl = sys.modules["matplotlib"]
+    if not hasattr(mpl, "pyplot"):
+        mpl.pyplot = types.ModuleType("matplotlib.pyplot")
+        sys.modules["matplotlib.pyplot"] = mpl.pyplot
+    import test_sdr_with_coding as H
+    cc = make_codec(T, 212, "1/3")
+    cc.inv_perm = np.argsort(cc.perm, kind="stable").astype(np.int32)
+    info = rng.integers(0, 2, cc.k_info)
+    coded = cc.encode(info)
+    syms = H.MODULATIONS["16QAM"]["mod"](coded).astype(np.complex64)
+    syms = (syms + 0.25 * (rng.standard_normal(syms.shape) + 1j * rng.standard_normal(syms.shape))).astype(np.complex64)
+    syms[[3, 77, 200]] = np.complex64(complex(np.nan, 0.5))
+    syms[[10, 11]] = np.complex64(complex(np.inf, -1.0))
+    syms[150] = np.complex64(complex(np.nan, np.nan))
+    llr = -H.compute_llr(syms, "16QAM", np.float64(0.1))
+    b, lf = _decode_capture(T, cc, llr)
+    out.update(chain_syms=syms, chain_llr=llr, chain_bits=b, chain_lfinal=lf, chain_inv=cc.inv_perm,
+               chain_noise_var=np.float64(0.1))
+    np.savez_compressed(os.path.join(OUT, "nonfinite.npz"), **out)
+
+
 def gen_demap():
     """compute_llr (test_sdr_with_coding.py:200-225) and the Gray mappers
     (:25-100; sdr_modem.py:101-220).  test_sdr_with_coding imports a stale
@@ -286,11 +388,15 @@ def gen_demap():
 def main():
     T = _import_reference()
     t0 = time.time()
+    if "--only" in sys.argv:   # one generator, e.g. --only nonfinite
+        globals()["gen_" + sys.argv[sys.argv.index("--only") + 1]](T)
+        return
     gen_tables(T); print("tables", time.time() - t0, flush=True)
     gen_encode(T); print("encode", time.time() - t0, flush=True)
     gen_siso(T); print("siso", time.time() - t0, flush=True)
     gen_demap(); print("demap", time.time() - t0, flush=True)
     gen_decode(T); print("decode", time.time() - t0, flush=True)
+    gen_nonfinite(T); print("nonfinite", time.time() - t0, flush=True)
 
 
 if __name__ == "__main__":

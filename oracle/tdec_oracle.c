@@ -191,12 +191,18 @@ static inline float lse4(float x0, float x1, float x2, float x3)
 float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy tests (bits) */
 float orc_lse4(float a, float b, float c, float d) { return lse4(a, b, c, d); }
 
+static void siso_exact(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
+                       const double *LaA, const double *LaB, const int32_t *tables, double sf,
+                       double *LeA, double *LeB);
+
 /* bcjr_max_log_map, dvb_rcs2_turbo.py:116-281 (algo 0); algo 1 = the build's
- * log-MAP (above): same passes, metrics in bits, max -> max*. */
+ * log-MAP (above): same passes, metrics in bits, max -> max*; algo 2 = exact
+ * f64 log-MAP (siso_exact, accuracy reference only). */
 void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
               const double *LaA, const double *LaB, const int32_t *tables, double sf, int algo,
               double *LeA, double *LeB)
 {
+    if (algo == 2) { siso_exact(N, LcA, LcB, LcW, LcY, LaA, LaB, tables, sf, LeA, LeB); return; }
     const int32_t *nx = tables, *ow = tables + 64, *oy = tables + 128, *ps = tables + 192, *pi = tables + 256;
     float *gamma = (float *)calloc((size_t)N * NS * 4, sizeof(float));
     float *alpha = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
@@ -333,6 +339,89 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
         if (a < -limit) a = -limit;
         if (b > limit) b = limit;
         if (b < -limit) b = -limit;
+        LeA[k] = a; LeB[k] = b;
+    }
+#undef GAM
+#undef ALP
+#undef BET
+    free(gamma); free(alpha); free(beta);
+}
+
+/* ------------------------------------------------------ exact log-MAP -- */
+/* Accuracy reference for the build-defined log-MAP (algo 2 of orc_siso /
+ * orc_decode): the same SISO structure (two passes per recursion from zero,
+ * state-0 normalisation, the reference's f64 extrinsic tail) with EVERY metric
+ * in f64 nats and the Jacobian logarithm max(a,b) + log1p(exp(-|a-b|)) of the
+ * historic _jacobian_log-22 evaluated in f64, without the
+ * f32 rounding of the branch metrics.  Not bit-compared with anything: the GPU's
+ * log-MAP (bits, f32 metrics, hardware exp2 / log2) is measured against it with
+ * stated tolerances (tests/test_gpu_logmap.py). */
+static inline double jac64(double a, double b)
+{
+    if (a != a) return b;   /* maxNum: a NaN operand is dropped */
+    if (b != b) return a;
+    const double m = a > b ? a : b, d = fabs(a - b);
+    if (d != d) return m;   /* inf - inf */
+    return m + log1p(exp(-d));
+}
+
+static void siso_exact(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
+                       const double *LaA, const double *LaB, const int32_t *tables, double sf,
+                       double *LeA, double *LeB)
+{
+    const int32_t *nx = tables, *ow = tables + 64, *oy = tables + 128, *ps = tables + 192, *pi = tables + 256;
+    double *gamma = (double *)calloc((size_t)N * NS * 4, sizeof(double));
+    double *alpha = (double *)calloc((size_t)(N + 1) * NS, sizeof(double));
+    double *beta = (double *)calloc((size_t)(N + 1) * NS, sizeof(double));
+#define GAM(k, s, i) gamma[((size_t)(k) * NS + (s)) * 4 + (i)]
+#define ALP(k, s) alpha[(size_t)(k) * NS + (s)]
+#define BET(k, s) beta[(size_t)(k) * NS + (s)]
+    for (int k = 0; k < N; ++k) {
+        const double in_A = (double)LcA[k] + LaA[k], in_B = (double)LcB[k] + LaB[k];
+        for (int s = 0; s < NS; ++s)
+            for (int inp = 0; inp < 4; ++inp) {
+                int bA = (inp >> 1) & 1, bB = inp & 1, bW = ow[s * 4 + inp], bY = oy[s * 4 + inp];
+                GAM(k, s, inp) = 0.5 * ((bA ? -in_A : in_A) + (bB ? -in_B : in_B) + (bW ? -(double)LcW[k] : (double)LcW[k]) +
+                                        (bY ? -(double)LcY[k] : (double)LcY[k]));
+            }
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1)
+            for (int s = 0; s < NS; ++s) ALP(0, s) = ALP(N, s);
+        for (int k = 0; k < N; ++k) {
+            for (int n = 0; n < NS; ++n) {
+                double mv = -INFINITY;
+                for (int idx = 0; idx < 4; ++idx) mv = jac64(mv, ALP(k, ps[n * 4 + idx]) + GAM(k, ps[n * 4 + idx], pi[n * 4 + idx]));
+                ALP(k + 1, n) = mv;
+            }
+            const double norm = ALP(k + 1, 0);
+            for (int s = 0; s < NS; ++s) ALP(k + 1, s) -= norm;
+        }
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1)
+            for (int s = 0; s < NS; ++s) BET(N, s) = BET(0, s);
+        for (int k = N - 1; k >= 0; --k) {
+            for (int s = 0; s < NS; ++s) {
+                double mv = -INFINITY;
+                for (int inp = 0; inp < 4; ++inp) mv = jac64(mv, BET(k + 1, nx[s * 4 + inp]) + GAM(k, s, inp));
+                BET(k, s) = mv;
+            }
+            const double norm = BET(k, 0);
+            for (int s = 0; s < NS; ++s) BET(k, s) -= norm;
+        }
+    }
+    for (int k = 0; k < N; ++k) {
+        double app[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (int s = 0; s < NS; ++s)
+            for (int inp = 0; inp < 4; ++inp) app[inp] = jac64(app[inp], ALP(k, s) + GAM(k, s, inp) + BET(k + 1, nx[s * 4 + inp]));
+        double a = (jac64(app[0], app[1]) - jac64(app[2], app[3])) - ((double)LcA[k] + LaA[k]);
+        double b = (jac64(app[0], app[2]) - jac64(app[1], app[3])) - ((double)LcB[k] + LaB[k]);
+        a *= sf; b *= sf;
+        if (a > 300.0) a = 300.0;
+        if (a < -300.0) a = -300.0;
+        if (b > 300.0) b = 300.0;
+        if (b < -300.0) b = -300.0;
         LeA[k] = a; LeB[k] = b;
     }
 #undef GAM

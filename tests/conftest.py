@@ -45,30 +45,31 @@ def G_demap():
     return golden("demap")
 
 
-@pytest.fixture(scope="session", autouse=True)
-def _oracle_log_map_primitives():
-    """On a GPU box, pin the oracle's log-MAP primitives (2^-t and log2 on their
-    bounded grids, oracle/tdec_oracle.c orc_set_trans) to this device's
-    v_exp_f32 / v_log_f32 outputs, so every log-MAP comparison is bit for bit;
-    tests/test_gpu_logmap.py checks the tables are faithful (within 1 ulp of the
-    correctly rounded values).  Without a GPU the oracle keeps the correctly
-    rounded primitives."""
+@pytest.fixture(scope="session")
+def _device_trans_tables():
+    """This device's v_exp_f32 / v_log_f32 outputs on the log-MAP primitives'
+    bounded grids (captured once per session), or None without a GPU."""
     try:
         import torch
         gpu = torch.cuda.is_available()
     except ImportError:
         gpu = False
     if not gpu:
-        yield None
-        return
+        return None
     from modulations_amd import dvb_rcs2_turbo as M
+    return M.capture_trans_tables(0)
+
+
+@pytest.fixture(scope="module")
+def trans_tables(_device_trans_tables):
+    """Pin the oracle's log-MAP primitives (oracle/tdec_oracle.c orc_set_trans)
+    to this device's instructions for the requesting module only, so its
+    GPU-vs-oracle log-MAP comparisons are bit for bit; every other module
+    (the CPU oracle tests included) sees the correctly rounded primitives
+    whether or not the box has a GPU.  tests/test_gpu_logmap.py checks the
+    tables are faithful (within 1 ulp of the correctly rounded values)."""
     from oracle import oracle as O
-    tabs = M.capture_trans_tables(0)
-    O.set_trans(tabs)
-    yield tabs
+    if _device_trans_tables is not None:
+        O.set_trans(_device_trans_tables)
+    yield _device_trans_tables
     O.set_trans(None)
-
-
-@pytest.fixture(scope="session")
-def trans_tables(_oracle_log_map_primitives):
-    return _oracle_log_map_primitives

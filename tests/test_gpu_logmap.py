@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("trans_tables")]
 
 from oracle import oracle as O  # noqa: E402
 from modulations_amd import demap as D  # noqa: E402

@@ -8,7 +8,7 @@ from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
 torch = pytest.importorskip("torch")
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("trans_tables")]
 
 from oracle import oracle as O  # noqa: E402
 from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402

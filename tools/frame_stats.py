@@ -32,7 +32,8 @@ def main():
     llr = ((1 - 2.0 * coded) * 2 / n0 * np.sqrt(2) / np.sqrt(2)
            + rng.standard_normal(coded.shape) * np.sqrt(2 / n0)).astype(np.float32)   # BPSK-equivalent LLRs
     out = (C.c_ulonglong * 8)()
-    lib.tdec_frame_stats(out)
+    c.decode_batch(llr)            # creates the handle (HIP initialised), warms up
+    lib.tdec_frame_stats(out)      # reset
     c.decode_batch(llr)
     lib.tdec_frame_stats(out)
     sisos = 2 * c.iterations * B * 2          # SISOs x 2 directions

@@ -263,26 +263,60 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     const int len = max(0, min(Ls, N - g * Ls)), u0 = len ? g * Ls : 0;   // empty segments never run
     const unsigned long long all = nseg == 4 ? ~0ull : (1ull << (16 * nseg)) - 1;
     const lds_b *src = R.ev + (g == 0 ? nseg - 1 : g - 1) * 64 + 4 * L.lbl[0];   // the start of a re-run
-    // pass 1: every segment from zero (segment 0: the reference's start), then the
-    // re-runs from each predecessor's end until nothing changes
+    // pass 1, phase A: every segment from zero (segment 0: the reference's start)
     unsigned long long reached = fr_round<DIR, false>(R, L, g, lane, u0, len, all, 0.0f, 0);
     unsigned long long dirty = (reached << 16) & all;
-    while (dirty) {
+    // The first re-run round also starts the reference's second pass SPECULATIVELY:
+    // group 0 (idle in the re-runs) runs from the last segment's phase-A end
+    // vector.  If that round leaves pass 1 complete and the last segment's end
+    // unchanged, that start was alpha1[N] / beta1[0] and the second pass goes on
+    // from this round's state; otherwise the second pass restarts below from the
+    // verified end vector.  (Merging against whatever segment 0 holds is exact
+    // either way: a stored segment is always one consistent trajectory.)
+    const unsigned long long G0 = 0xFFFFull, GL = 0xFFFFull << (16 * (nseg - 1));
+    bool spec = false, broken = false;
+    if (dirty) {
 #if TDEC_FR_STATS
         if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
-        dirty = (reached << 16) & all;
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty | G0, lds_ld(src), 1);
+        const unsigned long long r1 = reached & ~G0;
+        spec = !(r1 & GL);              // the last segment's end vector did not change
+        dirty = (r1 << 16) & all;
+        if (!dirty && spec) {
+            dirty = (reached & G0) << 16 & all;   // pass 1 done: the second pass continues
+        } else {
+            spec = false;
+            // if group 0 ran to its end, ev[0] and segment 0 hold the speculative
+            // trajectory while segment 1 still holds the pass-1 one: the chain of
+            // end vectors is broken at segment 0 until segment 1 re-runs
+            broken = (reached & G0) != 0;
+        }
+        // the remaining pass-1 rounds
+        while (!spec && dirty) {
+#if TDEC_FR_STATS
+            if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
+#endif
+            reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
+            dirty = (reached << 16) & all;
+        }
     }
-    // pass 2 from the pass-1 end vector (alpha1[N] / beta1[0]) at segment 0
-    dirty = 0xFFFFull;
-    do {
+    // the second pass (from alpha1[N] / beta1[0] at segment 0) unless the
+    // speculative start was right, then its remaining rounds
+    if (!spec) {
+#if TDEC_FR_STATS
+        if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
+#endif
+        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, G0, lds_ld(src), 2);
+        dirty = ((reached & G0) || broken) ? (G0 << 16) & all : 0ull;
+    }
+    while (dirty) {
 #if TDEC_FR_STATS
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
         reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 2);
         dirty = (reached << 16) & all;
-    } while (dirty);
+    }
 }
 
 // ---- inputs / outputs of one SISO -------------------------------------------------------

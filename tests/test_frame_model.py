@@ -129,16 +129,39 @@ def frame_recursion(pm, beta):
         ev[g][lbl[ln % 4]] = v
         return True
 
-    def rounds(dirty, src_of):
-        while dirty:
-            stats["rounds"] += 1
-            starts = {g: ev[src_of(g)].copy() for g in dirty}
-            reached = [g for g in dirty if run(g, starts[g], True)]
-            dirty = [g + 1 for g in reached if g + 1 < nseg]
+    src_of = lambda g: nseg - 1 if g == 0 else g - 1     # noqa: E731
+
+    def one_round(dirty):
+        stats["rounds"] += 1
+        starts = {g: ev[src_of(g)].copy() for g in dirty}   # read before any group writes its end
+        return [g for g in dirty if run(g, starts[g], True)]
 
     reached = [g for g in range(nseg) if run(g, np.zeros(16, np.float32), False)]
-    rounds([g + 1 for g in reached if g + 1 < nseg], lambda g: g - 1)
-    rounds([0], lambda g: nseg - 1 if g == 0 else g - 1)
+    dirty = [g + 1 for g in reached if g + 1 < nseg]
+    spec = broken = False
+    if dirty:
+        # first re-run round + the second pass started speculatively on group 0
+        reached = one_round([0] + dirty)
+        r1 = [g for g in reached if g != 0]
+        spec = (nseg - 1) not in r1
+        dirty = [g + 1 for g in r1 if g + 1 < nseg]
+        if not dirty and spec:
+            dirty = [1] if 0 in reached and nseg > 1 else []
+        else:
+            spec = False
+            # group 0 ran to its end: ev[0] and segment 0 now hold the speculative
+            # trajectory, segment 1 still the pass-1 one -- the chain is broken at 0
+            broken = 0 in reached and nseg > 1
+        while not spec and dirty:
+            reached = one_round(dirty)
+            dirty = [g + 1 for g in reached if g + 1 < nseg]
+    if not spec:
+        reached = one_round([0])
+        dirty = [1] if (0 in reached or broken) and nseg > 1 else []
+    while dirty:
+        reached = one_round(dirty)
+        dirty = [g + 1 for g in reached if g + 1 < nseg]
+    stats["spec"], stats["broken"] = spec, broken
     return st, stats
 
 
@@ -202,3 +225,22 @@ def test_segment_rounds_never_merging(beta):
     st, stats = frame_recursion(pm, beta)
     ref = reference_two_pass(pm, beta)
     np.testing.assert_array_equal(st, ref)
+
+
+def test_segment_rounds_random_sweep_covers_every_path():
+    """Random block lengths and metric scales: every control path of the rounds
+    (speculative second pass kept, dropped, dropped with the chain broken at
+    segment 0) is taken, and every result equals the serial two passes."""
+    rng = np.random.default_rng(2025)
+    seen = set()
+    for trial in range(120):
+        N = int(rng.integers(9, 90)) if trial % 3 else int(rng.integers(300, 420))
+        scale = float(10 ** rng.uniform(-3, 1))
+        pm = _pm(rng, N, scale)
+        if trial % 7 == 0:
+            pm[rng.integers(0, N)] = np.nan
+        beta = bool(trial % 2)
+        st, stats = frame_recursion(pm, beta)
+        np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
+        seen.add((stats["spec"], stats["broken"]))
+    assert {(True, False), (False, False), (False, True)} <= seen, seen

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 profile of one bench configuration: bench line + kernel trace + PMC passes
-#   tools/prof_r03.sh <tag> <bench args...>
+#   tools/prof_config.sh <tag> <bench args...>
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 TAG=$1

@@ -58,6 +58,26 @@ struct DevBuf {
     }
 };
 
+// Page-locked host staging for the small host-pointer calls (grown on demand).
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return 0;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return fail(TDEC_ENOMEM, "hipHostMalloc failed");
+        cap = bytes;
+        return 0;
+    }
+    void release() {
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 // A device buffer built from physical chunks mapped into one virtual range in a
 // shuffled order (HIP virtual memory management): the physical placement of the
 // decoder workspace is scattered BY CONSTRUCTION instead of by the placement
@@ -327,6 +347,7 @@ struct tdec_ctx {
     DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
     int cap_batch = 0;
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
+    PinBuf pin;                        // page-locked staging of the small host-pointer calls
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
@@ -585,6 +606,7 @@ void tdec_destroy(tdec_t *h) {
     h->h_bits.release();
     h->h_lf.release();
     h->h_misc.release();
+    h->pin.release();
     h->cons.buf.release();
     h->spl_ck.release();
     h->planes_w.release();
@@ -936,6 +958,7 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
 // stages every copy through its own pinned buffer on the CPU, which caps the
 // path at the host's staging rate; host buffers from tdec_host_alloc (or
 // registered by the caller) go straight to the DMA engines.
+constexpr size_t SMALL_CALL_BYTES = 16u << 20;
 struct EventPair {
     hipEvent_t e[2] = {nullptr, nullptr};
     int create() {
@@ -960,6 +983,33 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
     const int C = (int)std::min<long>(B, chunk);
     const long n_chunks = (B + C - 1) / C;
+    // Small calls (one chunk, <= SMALL_CALL_BYTES of traffic; decode() per frame is
+    // 12 KB in and 6 KB out): one page-locked staging buffer, one DMA each way on
+    // the handle's stream, no events -- the pageable copies' runtime staging and
+    // the pipeline's event setup were most of a per-frame call.
+    const size_t in_b = (size_t)B * llr_stride * sizeof(float), bits_b = (size_t)B * 2 * h->N * sizeof(int32_t),
+                 lf_b = lfinal ? (size_t)B * 2 * h->N * sizeof(double) : 0;
+    if (n_chunks == 1 && in_b + bits_b + lf_b <= SMALL_CALL_BYTES) {
+        int rc = tdec_reserve(h, B);
+        if (!rc) rc = h->h_llr.ensure(in_b);
+        if (!rc) rc = h->h_bits.ensure(bits_b);
+        if (!rc && lfinal) rc = h->h_lf.ensure(lf_b);
+        if (!rc) rc = h->pin.ensure(in_b + bits_b + lf_b);
+        if (rc) return rc;
+        DrainOnExit drain{h->stream, nullptr};
+        char *pin = (char *)h->pin.p;
+        std::memcpy(pin, llr, in_b);
+        HIPCHK(hipMemcpyAsync(h->h_llr.p, pin, in_b, hipMemcpyHostToDevice, h->stream));
+        if ((rc = tdec_decode_batch_dev(h, B, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
+                                        lfinal ? (double *)h->h_lf.p : nullptr, h->stream)))
+            return rc;
+        HIPCHK(hipMemcpyAsync(pin + in_b, h->h_bits.p, bits_b, hipMemcpyDeviceToHost, h->stream));
+        if (lfinal) HIPCHK(hipMemcpyAsync(pin + in_b + bits_b, h->h_lf.p, lf_b, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        std::memcpy(bits, pin + in_b, bits_b);
+        if (lfinal) std::memcpy(lfinal, pin + in_b + bits_b, lf_b);
+        return 0;
+    }
     const int nbuf = n_chunks > 1 ? 2 : 1;
     int rc = tdec_reserve(h, C);
     const size_t row_b = (size_t)2 * h->N, llr_c = (size_t)C * llr_stride, bits_c = (size_t)C * row_b;
@@ -1076,15 +1126,32 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     double *deA = (double *)(base + 4 * cf + 2 * cd), *deB = (double *)(base + 4 * cf + 3 * cd);
     hipStream_t s = h->stream;
     const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
+    // small calls (a bcjr_max_log_map call is one row): the six inputs packed into one
+    // page-locked buffer laid out as the device staging, one DMA each way
+    const bool small = B <= C && 4 * cf + 4 * cd <= SMALL_CALL_BYTES;
+    if (small) {
+        if (int rc = h->pin.ensure(4 * cf + 4 * cd)) return rc;
+    }
     for (long r0 = 0; r0 < B; r0 += C) {
         const int n = (int)std::min<long>(C, B - r0), nwv = n_tiles_of(n);
         const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(float), nd = (size_t)n * N * sizeof(double);
-        HIPCHK(hipMemcpyAsync(dA, LcA + o, nf, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dB, LcB + o, nf, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dW, LcW + o, nf, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dY, LcY + o, nf, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(daA, LaA + o, nd, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
+        if (small) {
+            char *pin = (char *)h->pin.p;
+            std::memcpy(pin, LcA + o, nf);
+            std::memcpy(pin + cf, LcB + o, nf);
+            std::memcpy(pin + 2 * cf, LcW + o, nf);
+            std::memcpy(pin + 3 * cf, LcY + o, nf);
+            std::memcpy(pin + 4 * cf, LaA + o, nd);
+            std::memcpy(pin + 4 * cf + cd, LaB + o, nd);
+            HIPCHK(hipMemcpyAsync(base, pin, 4 * cf + 2 * cd, hipMemcpyHostToDevice, s));
+        } else {
+            HIPCHK(hipMemcpyAsync(dA, LcA + o, nf, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(dB, LcB + o, nf, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(dW, LcW + o, nf, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(dY, LcY + o, nf, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(daA, LaA + o, nd, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
+        }
         SisoArgs a{n, h->N, nwv, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
         const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
         if (fr) {
@@ -1101,9 +1168,17 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
         else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
         else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(LeA + o, deA, nd, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(LeB + o, deB, nd, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        if (small) {
+            char *pin = (char *)h->pin.p + 4 * cf + 2 * cd;
+            HIPCHK(hipMemcpyAsync(pin, deA, 2 * cd, hipMemcpyDeviceToHost, s));   // deB follows deA
+            HIPCHK(hipStreamSynchronize(s));
+            std::memcpy(LeA + o, pin, nd);
+            std::memcpy(LeB + o, pin + cd, nd);
+        } else {
+            HIPCHK(hipMemcpyAsync(LeA + o, deA, nd, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(LeB + o, deB, nd, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
     }
     return mark_used(h, s);
 }

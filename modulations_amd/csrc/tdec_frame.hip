@@ -167,7 +167,8 @@ struct FrRec {
 #define TDEC_FR_STATS 0
 #endif
 #if TDEC_FR_STATS
-__device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, pass 2; rounds: fix-up, pass 2
+__device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, pass 2; rounds: fix-up, pass 2;
+                                               // s_memrealtime ticks (100 MHz) of phases P, R, E (thread 0)
 #endif
 
 // One round of the groups in `run` (wave-uniform lane mask), each from its start
@@ -401,6 +402,9 @@ template <class In, class Out>
 __device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo, int N, double sf) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     lds_b *pmt = sm + Lo.pmt;
+#if TDEC_FR_STATS
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // P: pair maxima of every position
     for (int k = tid; k < N; k += FR_BLOCK) {
         double iA, iB;
@@ -414,10 +418,16 @@ __device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo
         d[1] = f4v{pm[1][0], pm[1][1], pm[1][2], pm[1][3]};
     }
     __syncthreads();
+#if TDEC_FR_STATS
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+#endif
     // R: alpha on wave 0, beta on wave 1
     if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
     else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + 256, sm + Lo.sink + 512, N}, lane);
     __syncthreads();
+#if TDEC_FR_STATS
+    const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+#endif
     // E: extrinsic of every position anyone reads
     const int M = out.count(N);
     for (int i = tid; i < M; i += FR_BLOCK) {
@@ -440,6 +450,14 @@ __device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo
         out.store(k, leA, leB, la, lb);
     }
     __syncthreads();
+#if TDEC_FR_STATS
+    if (tid == 0) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_fr_stats[5], t1 - t0);
+        atomicAdd(&g_fr_stats[6], t2 - t1);
+        atomicAdd(&g_fr_stats[7], t3 - t2);
+    }
+#endif
 }
 
 struct FrArgs {

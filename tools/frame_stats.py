@@ -40,7 +40,8 @@ def main():
     res = {"N": n, "rate": rate, "ebn0": ebn0, "B": B,
            "steps_per_siso_dir": {"phaseA": 4 * out[0] / sisos, "fixup": 4 * out[1] / sisos,
                                   "pass2": 4 * out[2] / sisos},
-           "rounds_per_siso_dir": {"fixup": out[3] / sisos, "pass2": out[4] / sisos}}
+           "rounds_per_siso_dir": {"fixup": out[3] / sisos, "pass2": out[4] / sisos},
+           "us_per_siso": {ph: round(out[i] * 0.01 / (sisos // 2), 3) for i, ph in ((5, "P"), (6, "R"), (7, "E"))}}
     print(json.dumps(res))
 
 

@@ -150,6 +150,16 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
  * n_out = the reference encoder's output length. */
 int tdec_encode_dev(tdec_t *h, int B, const uint8_t *d_bits, uint8_t *d_coded, void *stream);
 long tdec_encoded_len(const tdec_t *h);
+/* The drop-in's DVBRCS2_Turbo.encode (dvb_rcs2_turbo.py:404-462) on the HOST
+ * (compiled; needs no handle and no GPU): B rows of int32 info bits [2N]
+ * (A, B interleaved; row stride bits_stride) -> int32 coded rows (stride
+ * out_stride >= the returned length).  punct: [4][4] pattern rows W1, Y1, W2, Y2
+ * as tdec_create; perm: int32[N] (any values in [0, N)).  An input
+ * (A << 1) | B outside [-4, 3] is TDEC_ESHORT (numpy's IndexError in the
+ * reference's next_state lookup; -4..-1 wrap as numpy's negative indices).
+ * Returns the coded length per row (> 0) or a negative error code. */
+long tdec_encode_host(int n_couples, int period, const uint8_t *punct, const int32_t *perm, long B,
+                      const int32_t *bits, long bits_stride, int32_t *out, long out_stride);
 
 /* ---- counter-based workload generation (not a reference API) ----
  * Codeword c of a batch has the GLOBAL index cw0 + c; its info bits and its

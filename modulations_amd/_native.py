@@ -28,7 +28,7 @@ EXPORTS = (
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
     "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
-    "tdec_host_alloc", "tdec_host_free",
+    "tdec_host_alloc", "tdec_host_free", "tdec_encode_host",
 )
 
 _lib = None
@@ -78,6 +78,8 @@ def _declare(L):
     L.tdec_host_alloc.argtypes = [C.c_size_t, C.POINTER(_vp)]
     L.tdec_host_free.argtypes = [_vp]
     L.tdec_host_free.restype = None
+    L.tdec_encode_host.argtypes = [C.c_int, C.c_int, _vp, _vp, C.c_long, _vp, C.c_long, _vp, C.c_long]
+    L.tdec_encode_host.restype = C.c_long
     for name in EXPORTS:
         f = getattr(L, name)
         if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",

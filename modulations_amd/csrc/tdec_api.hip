@@ -620,6 +620,72 @@ void tdec_destroy(tdec_t *h) {
 }
 
 long tdec_llr_len(const tdec_t *h) { return h ? h->llr_len : TDEC_EINVAL; }
+
+long tdec_encode_host(int n_couples, int period, const uint8_t *punct, const int32_t *perm, long B,
+                      const int32_t *bits, long bits_stride, int32_t *out, long out_stride) {
+    const int N = n_couples;
+    if (N <= 0 || period < 1 || period > 4 || !punct || !perm || B < 0 || (B > 0 && (!bits || !out)))
+        return fail(TDEC_EINVAL, "bad encode arguments");
+    long n_out = 0;
+    for (int i = 0; i < N; ++i) {
+        n_out += 2;
+        for (int r = 0; r < 4; ++r) n_out += punct[r * 4 + i % period] ? 1 : 0;
+    }
+    if (B > 0 && (bits_stride < 2L * N || out_stride < n_out)) return fail(TDEC_EINVAL, "encode row strides too short");
+    for (int k = 0; k < N; ++k)
+        if (perm[k] < 0 || perm[k] >= N) return fail(TDEC_EINVAL, "perm entry out of range");
+    // circular-state table S_c = solve((I + G^N), Z) (:414-417), as tdec_create
+    int G[16] = {0};
+    G[0 * 4 + 2] = G[0 * 4 + 3] = G[1 * 4 + 0] = G[2 * 4 + 1] = G[3 * 4 + 2] = 1;
+    int res[16], base[16], circ[16];
+    for (int i = 0; i < 16; ++i) res[i] = (i % 5) == 0;
+    std::memcpy(base, G, sizeof base);
+    for (long pw = N; pw > 0; pw /= 2) {
+        if (pw % 2 == 1) mat_mul_gf2(res, base, res);
+        mat_mul_gf2(base, base, base);
+    }
+    for (int z = 0; z < 16; ++z) circ[z] = solve_circ(res, z);
+    std::vector<int> in1(N), in2(N);
+    std::vector<uint8_t> w1(N), y1(N), w2(N), y2(N);
+    // one RSC component (:404-429): zero-state pass, circular start, encode pass
+    auto component = [&](const std::vector<int> &in, std::vector<uint8_t> &W, std::vector<uint8_t> &Y) {
+        int s = 0;
+        for (int i = 0; i < N; ++i) s = t_next(s, in[i]);
+        s = circ[s];
+        for (int i = 0; i < N; ++i) {
+            W[i] = (uint8_t)t_ow(s, in[i]);
+            Y[i] = (uint8_t)t_oy(s, in[i]);
+            s = t_next(s, in[i]);
+        }
+    };
+    for (long b = 0; b < B; ++b) {
+        const int32_t *x = bits + b * bits_stride;
+        for (int i = 0; i < N; ++i) {
+            // (A << 1) | B indexes next_state[state, :]: numpy wraps -4..-1, raises otherwise
+            const int32_t v = (int32_t)((uint32_t)x[2 * i] << 1) | x[2 * i + 1];
+            if (v < -4 || v > 3) return fail(TDEC_ESHORT, "index out of bounds for the next_state lookup (info bits must be 0/1)");
+            in1[i] = v & 3;
+        }
+        for (int i = 0; i < N; ++i) {   // A[perm], B[perm] (:447-449)
+            const int32_t *q = x + 2 * perm[i];
+            in2[i] = (int)(((int32_t)((uint32_t)q[0] << 1) | q[1]) & 3);
+        }
+        component(in1, w1, y1);
+        component(in2, w2, y2);
+        int32_t *o = out + b * out_stride;
+        long j = 0;
+        for (int i = 0; i < N; ++i) {   // puncture / multiplex (:451-460)
+            const int p = i % period;
+            o[j++] = x[2 * i];
+            o[j++] = x[2 * i + 1];
+            if (punct[0 * 4 + p]) o[j++] = w1[i];
+            if (punct[1 * 4 + p]) o[j++] = y1[i];
+            if (punct[2 * 4 + p]) o[j++] = w2[i];
+            if (punct[3 * 4 + p]) o[j++] = y2[i];
+        }
+    }
+    return n_out;
+}
 long tdec_encoded_len(const tdec_t *h) { return h ? h->enc_len : TDEC_EINVAL; }
 
 size_t tdec_planes_bytes(const tdec_t *h, int B) {

@@ -1967,7 +1967,7 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
 // All BPS LLRs of one symbol, reference sign (positive -> bit 1) unless
 // c.sign < 0.  Streams over the M points keeping a running min per bit and
 // label value, so no distance array is materialised.
-template <typename T, int BPS, bool FIN, int M = (1 << BPS)>
+template <typename T, int BPS, bool FIN, int M = (1 << BPS), int UNROLL = (M <= 16 ? M : 8)>
 __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     T m0[BPS], m1[BPS];
     bool n0[BPS], n1[BPS];
@@ -1977,7 +1977,7 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
         n0[b] = n1[b] = false;
     }
     // M is the full label space; a table with fewer points (c.M < M) stops early.
-#pragma unroll (M <= 16 ? M : 8)
+#pragma unroll UNROLL
     for (int m = 0; m < M; ++m) {
         if (M > 2 && m >= c.M) break;
         const T a = FIN ? cabs_fin<T>(sr - cons[2 * m], si - cons[2 * m + 1]) : cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
@@ -2267,6 +2267,9 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 // (:469-474; the harness pads to n_coded, test_sdr_with_coding.py:474-478).
 // src[c*N + k] = LLR index of plane component c (X.xyzw, -, -, Z.xy) or -1;
 // off[k] = first LLR index of couple k (off[N] = n_llr).
+#ifndef TDEC_DM_LEAN
+#define TDEC_DM_LEAN 1
+#endif
 constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
@@ -2277,6 +2280,17 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                                                        const int *__restrict__ off, long n_avail, float *planes) {
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
+    // TDEC_DM_LEAN (round 4, square 16 / 64 / 256QAM): phase 1 runs only the fast
+    // exact search (per-axis / Gray positions) and queues the symbols it declines
+    // (near ties, non-finite, a non-separable table); a second loop gives those
+    // the exact scan.  Inline in one loop, the fallback's registers were the
+    // kernel's (256QAM: 142 VGPRs and 289 spilled SGPRs against 88 and none for
+    // the Gray search alone).  Same planes: every path returns the scan's LLRs.
+    constexpr bool LEAN = TDEC_DM_LEAN && BPS >= 4 && BPS % 2 == 0;
+    constexpr int QW = LEAN ? (WAVE * (DM_MAXL / BPS + 2) + 31) / 32 : 1;   // bitmask words over the items
+    __shared__ unsigned fq[QW];
+    if constexpr (LEAN)
+        for (int i = threadIdx.x; i < QW; i += BLOCK) fq[i] = 0u;
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + DM_KC - 1) / DM_KC;
     const long tile = blockIdx.x / chunks;
@@ -2300,7 +2314,19 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         if (cw >= B || s >= S) continue;
         const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
         double v[BPS];
-        demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+        if constexpr (LEAN) {
+            // the fast exact search: Gray positions (64 / 256QAM) or the per-axis search (16QAM)
+            bool ok;
+            if constexpr (BPS >= 6) ok = c.sep == 2 && sym_llrs_gray<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+            else ok = c.sep && sym_llrs_sep<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+            if (!ok) {
+                const int it = lane * ns + si;   // < QW * 32
+                atomicOr(&fq[it >> 5], 1u << (it & 31));
+                continue;
+            }
+        } else {
+            demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+        }
 #pragma unroll
         for (int b = 0; b < BPS; ++b) {
             const long j = s * BPS + b;
@@ -2308,6 +2334,22 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         }
     }
     __syncthreads();
+    if constexpr (LEAN) {
+        for (int it = threadIdx.x; it < WAVE * ns; it += BLOCK) {
+            if (!((fq[it >> 5] >> (it & 31)) & 1u)) continue;
+            const int ln = it / ns, sx = it - ln * ns;
+            const long cw = tile * WAVE + ln, s = s0 + sx;
+            const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+            double v[BPS];
+            sym_llrs_scan<T, BPS, false, (1 << BPS), (BPS <= 4 ? 16 : 1)>((T)z.x, (T)z.y, cons, c, v);
+#pragma unroll
+            for (int b = 0; b < BPS; ++b) {
+                const long j = s * BPS + b;
+                if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
+            }
+        }
+        __syncthreads();
+    }
     float *base = planes + tile * tile_floats(N);
     for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
         const int lane = t & (WAVE - 1);

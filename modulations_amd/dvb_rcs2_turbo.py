@@ -150,40 +150,34 @@ class DVBRCS2_Turbo:
         return self._h
 
     # -- encode (host; :404-462) -----------------------------------------------------
-    def _encode_component(self, A, B):
-        state = 0
-        for i in range(self.N):
-            state = self.next_state[state, (A[i] << 1) | B[i]]
-        if self._circ is None:
-            self._circ = _t.circular_state_table(self.N, self.G_matrix)
-        state = int(self._circ[state])
-        W = np.zeros(self.N, dtype=np.int32)
-        Y = np.zeros(self.N, dtype=np.int32)
-        for i in range(self.N):
-            inp = (A[i] << 1) | B[i]
-            W[i] = self.out_W[state, inp]
-            Y[i] = self.out_Y[state, inp]
-            state = self.next_state[state, inp]
-        return W, Y
-
     def encode(self, bits):
-        """Encode bits into a DVB-RCS2 turbo codeword (reference :431-462)."""
+        """Encode bits into a DVB-RCS2 turbo codeword (reference :431-462), by the
+        library's compiled host encoder (tdec_encode_host: no GPU needed)."""
         bits = np.array(bits, dtype=np.int32)
-        A = bits[0::2]
-        B = bits[1::2]
-        W1, Y1 = self._encode_component(A, B)
-        W2, Y2 = self._encode_component(A[self.perm], B[self.perm])
-        coded = []
-        period = self.punct['period']
-        for i in range(self.N):
-            p = i % period
-            coded.append(A[i])
-            coded.append(B[i])
-            if self.punct['W1'][p]: coded.append(W1[i])
-            if self.punct['Y1'][p]: coded.append(Y1[i])
-            if self.punct['W2'][p]: coded.append(W2[i])
-            if self.punct['Y2'][p]: coded.append(Y2[i])
-        return np.array(coded, dtype=np.int32)
+        if bits.ndim != 1 or bits.shape[0] < 2 * self.N:
+            raise IndexError(f"index {bits.shape[0] if bits.ndim else 0} is out of bounds for axis 0 "
+                             f"with size {bits.shape[0] if bits.ndim else 0}")
+        return self.encode_batch(bits[None, :2 * self.N])[0]
+
+    def encode_batch(self, bits):
+        """encode() of B rows at once: int [B, 2N] -> int32 [B, n_out]."""
+        bits = np.ascontiguousarray(np.asarray(bits, dtype=np.int32))
+        if bits.ndim != 2 or bits.shape[1] < 2 * self.N:
+            raise ValueError("encode_batch takes a [B, 2N] array")
+        B = bits.shape[0]
+        out = np.zeros((B, self._enc_len()), np.int32)
+        pm = np.ascontiguousarray(_t.puncture_matrix(self.punct))
+        perm = np.ascontiguousarray(self.perm, np.int32)
+        rc = _n.lib().tdec_encode_host(self.N, self.punct["period"], _n.ptr(pm), _n.ptr(perm), B, _n.ptr(bits),
+                                       bits.shape[1], _n.ptr(out), out.shape[1])
+        if rc < 0:
+            _n.check(int(rc))
+        return out
+
+    def _enc_len(self):
+        p = self.punct
+        return sum(2 + p["W1"][i % p["period"]] + p["Y1"][i % p["period"]] + p["W2"][i % p["period"]]
+                   + p["Y2"][i % p["period"]] for i in range(self.N))
 
     # -- decode (:464-537) -----------------------------------------------------------
     def decode(self, llr):

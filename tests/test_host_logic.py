@@ -52,6 +52,31 @@ def test_host_encode_matches_reference(G_encode):
             assert np.array_equal(c.encode(b), cw)
 
 
+@pytest.mark.parametrize("n", [48, 64, 212, 220, 424, 752, 848])
+@pytest.mark.parametrize("rate", ["1/3", "1/2", "2/3", "3/4"])
+def test_compiled_host_encode_matches_oracle(n, rate):
+    """DVBRCS2_Turbo.encode / encode_batch run tdec_encode_host (compiled, no
+    GPU): equal to the oracle's restatement of :404-462 for random rows, the
+    reference's extra-bits and index-wrap behaviour kept."""
+    from oracle import oracle as O
+    c = M.DVBRCS2_Turbo(n, rate)
+    t, G = O.trellis()
+    pm = T.puncture_matrix(c.punct)
+    rng = np.random.default_rng(n)
+    info = rng.integers(0, 2, (5, c.k_info)).astype(np.int32)
+    got = c.encode_batch(info)
+    for b in range(5):
+        assert np.array_equal(got[b], O.encode(info[b], n, c.punct["period"], pm, c.perm, t, G))
+        assert np.array_equal(c.encode(info[b]), got[b])
+    assert np.array_equal(c.encode(np.concatenate([info[0], [1, 0, 1]])), got[0])   # extra bits ignored
+    with pytest.raises(IndexError):
+        c.encode(info[0][:-2])
+    bad = info[0].copy()
+    bad[4] = 2                                       # (2 << 1) | B = 4: numpy IndexError
+    with pytest.raises(IndexError):
+        c.encode(bad)
+
+
 @pytest.mark.parametrize("rate", ["1/3", "1/2", "2/3", "3/4"])
 def test_puncture_walk(rate):
     p = T.PUNCTURE_PATTERNS[rate]

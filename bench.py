@@ -283,6 +283,8 @@ def main():
     device = torch.device("cuda", dev_idx)
 
     codec = M.DVBRCS2_Turbo(args.n, args.rate, 8, algo=args.algo, device=device.index)
+    if dist:   # every rank must decode with the same de-interleaver (sharding.check_same_interleaver)
+        Sh.check_same_interleaver(codec.inv_perm, tdist, device if args.dist_backend == "nccl" else torch.device("cpu"))
     bps = D.MODULATIONS[args.mod]["bps"]
     cons = D.constellation(args.mod)
     B = args.batch

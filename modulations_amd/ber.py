@@ -39,11 +39,17 @@ def ebn0_seed(base_seed, ebn0_db):
     return (int(base_seed) * 1_000_003 + int(round(float(ebn0_db) * 1000)) * 7919) & 0xFFFFFFFFFFFFFFFF
 
 
-def sweep_config(a):
-    """What a results file is keyed on (argparse namespace -> dict)."""
-    return {"generator": GENERATOR, "mod": a.mod, "n_couples": int(a.n), "rate": a.rate, "algo": a.algo,
-            "iterations": int(a.iterations), "interleaver": a.interleaver, "codewords": int(a.codewords),
-            "seed": int(a.seed)}
+def sweep_config(a, inv_perm=None):
+    """What a results file is keyed on (argparse namespace -> dict), including the
+    digest of the inverse interleaver actually used (sharding.interleaver_digest:
+    the reference's default differs between numpy builds)."""
+    from .sharding import interleaver_digest
+    cfg = {"generator": GENERATOR, "mod": a.mod, "n_couples": int(a.n), "rate": a.rate, "algo": a.algo,
+           "iterations": int(a.iterations), "interleaver": a.interleaver, "codewords": int(a.codewords),
+           "seed": int(a.seed)}
+    if inv_perm is not None:
+        cfg["inv_perm_digest"] = interleaver_digest(inv_perm)
+    return cfg
 
 
 def load_resume(path, cfg):
@@ -124,7 +130,9 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.all_on_device0 and world > 1 and a.dist_backend == "nccl":
         ap.error("--all-on-device0 puts several ranks on one GPU, which RCCL cannot do: add --dist-backend gloo")
-    cfg = sweep_config(a)
+    # the codec touches no GPU until its first call: its inv_perm keys the sweep
+    host_codec = M.DVBRCS2_Turbo(a.n, a.rate, a.iterations, algo=a.algo, interleaver=a.interleaver)
+    cfg = sweep_config(a, host_codec.inv_perm)
     try:
         done = load_resume(a.out, cfg)
     except ValueError as e:
@@ -141,6 +149,8 @@ def main(argv=None):
     device = torch.device("cuda", dev_idx)
     codec = M.DVBRCS2_Turbo(a.n, a.rate, a.iterations, algo=a.algo, interleaver=a.interleaver,
                             device=device.index)
+    if world > 1:   # every rank must decode with the same de-interleaver
+        S.check_same_interleaver(codec.inv_perm, dist, device if a.dist_backend == "nccl" else "cpu")
     pipe = DevicePipeline(codec, a.mod, a.batch, device)
     results = list(done.values())
     for e in parse_points(a.ebn0):

@@ -11,7 +11,34 @@ not depend on which rank or batch generates it.
 """
 from __future__ import annotations
 
+import hashlib
+
 SEED_STRIDE = 1_000_003
+
+
+def interleaver_digest(inv_perm):
+    """63-bit digest of an inverse interleaver (int32 bytes).  The reference's
+    default inv_perm = np.argsort(perm) breaks the ties of its non-bijective perm
+    by the host numpy's sort path, so ranks on different hosts
+    can hold different de-interleavers: the digest goes into a sweep's config
+    key and is compared across ranks before any codeword is decoded."""
+    import numpy as np
+    b = np.ascontiguousarray(np.asarray(inv_perm, dtype=np.int32)).tobytes()
+    return int.from_bytes(hashlib.sha256(b).digest()[:8], "little") >> 1
+
+
+def check_same_interleaver(inv_perm, dist=None, device="cpu"):
+    """Raise if the ranks of the process group do not all hold this inv_perm
+    (one all-reduce of [d, -d] with MAX: equal iff max d == min d)."""
+    if dist is None or not dist.is_available() or not dist.is_initialized():
+        return
+    import torch
+    d = interleaver_digest(inv_perm)
+    t = torch.tensor([d, -d], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if int(t[0]) != -int(t[1]):
+        raise RuntimeError("ranks hold different inverse interleavers (np.argsort tie order differs between "
+                           "hosts): pin inv_perm ('stable', 'numpy-avx512' or an explicit array)")
 
 
 def shard_range(total, world, rank):

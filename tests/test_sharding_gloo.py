@@ -87,3 +87,39 @@ def test_two_rank_gloo_equals_single_process():
         assert tmax == 2.0
     bits = np.concatenate([r[2] for r in res])
     assert np.array_equal(bits, single_bits)
+
+
+def _inv_worker(rank, world, port, q, differ):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    inv = np.argsort(np.arange(48)[::-1], kind="stable").astype(np.int32)
+    if differ and rank == 1:
+        inv = inv.copy()
+        inv[[0, 1]] = inv[[1, 0]]        # another tie order on this "host"
+    try:
+        S.check_same_interleaver(inv, dist)
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, "mismatch" if "different inverse interleavers" in str(e) else repr(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("differ", [False, True])
+def test_ranks_must_share_the_inverse_interleaver(differ):
+    """the reference's default inv_perm depends on the host's numpy,
+    so a multi-host job checks that every rank holds the same one (bench.py and
+    ber.py call this before decoding; ber.py also keys its resume file on it)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inv_worker, args=(r, 2, port, q, differ)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == (["mismatch"] * 2 if differ else ["ok"] * 2)
+    assert S.interleaver_digest([1, 0, 2]) != S.interleaver_digest([0, 1, 2])

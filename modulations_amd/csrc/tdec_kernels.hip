@@ -58,10 +58,24 @@ __host__ __device__ constexpr int t_prev_i(int ns, int idx) {
 // instead of 0.5 (see the log-MAP section below).
 constexpr double LM_K = 0x1.71547652b82fep-1;     // 0.5 * log2(e)
 constexpr double LM_LN2 = 0x1.62e42fefa39efp-1;   // ln 2: bits -> nats
+// log-MAP (ALGO 1, round 4) uses the branch metric's two halves instead:
+// g = {U0, U1, V0, V1, 0...} with U0 = f32(hA + hB), U1 = f32(hA - hB),
+// V0 = f32(hW + hY), V1 = f32(hW - hY) (f64 sums rounded once, weights in bits):
+// a branch of input class c (A^B) and parity pair wy carries +-U_c + v(wy),
+// v = {V0, V1, -V1, -V0}, so a parallel pair's log-sum is v(wy) + max*(U_c, -U_c)
+// (2 max* per step instead of 8; see pair_jac).
 template <int ALGO = 0>
 __device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w, float y, float (&g)[8]) {
     constexpr double hw = ALGO ? LM_K : 0.5;
     const double hA = inA * hw, hB = inB * hw, hW = (double)w * hw, hY = (double)y * hw;
+    if constexpr (ALGO == 1) {
+        g[0] = (float)(hA + hB);
+        g[1] = (float)(hA + (-hB));
+        g[2] = (float)(hW + hY);
+        g[3] = (float)(hW + (-hY));
+        g[4] = g[5] = g[6] = g[7] = 0.0f;
+        return;
+    }
     const double l1[2] = {hA + hB, hA + (-hB)};
 #pragma unroll
     for (int bB = 0; bB < 2; ++bB)
@@ -185,19 +199,18 @@ __device__ __forceinline__ void pair_max(const float (&g)[8], float (&pm)[2][4])
         pm[1][wy] = fmaxf(g[4 + wy], -g[4 + 3 - wy]);    // g(A0 B1 wy), g(A1 B0 wy) = -g(A0 B1 ~wy)
     }
 }
-// log-MAP's pair values: max*(g(input 0), g(input 3)) and max*(g(input 1), g(input 2))
-// (jac is symmetric except for NaN operands, so the order is part of the definition)
+// log-MAP's pair values (round 4): the pair of class c and parity pair wy carries
+// +-U_c + v(wy), so its log-sum is v(wy) + C_c with C_c = max*(U_c, -U_c): two max*
+// per step (round 3 took one per pair, eight, from the rounded full branch metrics)
+__device__ __forceinline__ float lm_v(const float (&g)[8], int wy) {   // v = {V0, V1, -V1, -V0}
+    return wy == 0 ? g[2] : wy == 1 ? g[3] : wy == 2 ? -g[3] : -g[2];
+}
 __device__ __forceinline__ void pair_jac(const float (&g)[8], float (&pm)[2][4]) {
+    const float C0 = jac(g[0], -g[0]), C1 = jac(g[1], -g[1]);
 #pragma unroll
     for (int wy = 0; wy < 4; ++wy) {
-        if constexpr (TDEC_LM_PK) {
-            const f2 r = jac2(f2{g[wy], g[4 + wy]}, f2{-g[3 - wy], -g[4 + 3 - wy]});
-            pm[0][wy] = r.x;
-            pm[1][wy] = r.y;
-        } else {
-            pm[0][wy] = jac(g[wy], -g[3 - wy]);
-            pm[1][wy] = jac(g[4 + wy], -g[4 + 3 - wy]);
-        }
+        pm[0][wy] = lm_v(g, wy) + C0;
+        pm[1][wy] = lm_v(g, wy) + C1;
     }
 }
 __device__ __forceinline__ float pm_of(const float (&pm)[2][4], int s, int inp) {
@@ -388,25 +401,13 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
                     V[c][wy + 1] = lse4(x[1][0], x[1][1], x[1][2], x[1][3]);
                 }
             }
-        float app[4];
+        // app[inp] = +-U_c + X_c, X_c = lse4 over wy of (v(wy) + V[c][wy]): the two
+        // inputs of a class share X_c (round 4; round 3 took one lse4 per input)
+        float X[2];
 #pragma unroll
-        for (int inp = 0; inp < 4; inp += 2) {
-            float y[2][4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = (inp + h == 1 || inp + h == 2) ? 1 : 0;
-#pragma unroll
-                for (int wy = 0; wy < 4; ++wy) y[h][wy] = gam(g, LM_GROUPS.s[c][wy][0], inp + h) + V[c][wy];
-            }
-            if constexpr (TDEC_LM_PK) {
-                const f2 r = lse4x2(f2{y[0][0], y[1][0]}, f2{y[0][1], y[1][1]}, f2{y[0][2], y[1][2]}, f2{y[0][3], y[1][3]});
-                app[inp] = r.x;
-                app[inp + 1] = r.y;
-            } else {
-                app[inp] = lse4(y[0][0], y[0][1], y[0][2], y[0][3]);
-                app[inp + 1] = lse4(y[1][0], y[1][1], y[1][2], y[1][3]);
-            }
-        }
+        for (int c = 0; c < 2; ++c)
+            X[c] = lse4(lm_v(g, 0) + V[c][0], lm_v(g, 1) + V[c][1], lm_v(g, 2) + V[c][2], lm_v(g, 3) + V[c][3]);
+        const float app[4] = {g[0] + X[0], g[1] + X[1], -g[1] + X[1], -g[0] + X[0]};
         if constexpr (TDEC_LM_PK) {
             const f2 hi = jac2(f2{app[0], app[0]}, f2{app[1], app[2]}), lo = jac2(f2{app[2], app[1]}, f2{app[3], app[3]});
             LpA = hi.x - lo.x;

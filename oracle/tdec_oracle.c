@@ -122,13 +122,19 @@ static inline float maxlog_acc(float acc, float t) { return t > acc ? t : acc; }
  *                  S = fmaf(E(Mc - x_i), 256, S) over i in order from S = 0
  *   (Mc - 8 is exact: M rounded to the grid of Mc, the shift every term's
  *   E(Mc - x_i) * 256 = 2^(x_i - (Mc - 8)) was taken against).
- * Recursions: each state's two parallel branches first, pm = max*(g(lower
- * input), g(higher input)), then max*(a[p0] + pm, a[p0 + 8] + pm') over the two
- * predecessors in table order (beta: successor classes {0, 3} then {1, 2}).
+ * Branch metrics (round 4) in two halves, each an f64 sum rounded once:
+ * U0 = hA + hB, U1 = hA - hB, V0 = hW + hY, V1 = hW - hY (h = 0.5 log2(e) x
+ * the reference's f64 inputs); a branch of input class c = A^B and parity pair
+ * wy = 2W + Y carries +-U_c + v(wy), v = {V0, V1, -V1, -V0}.
+ * Recursions: each state's two parallel branches first -- their log-sum is
+ * pm = v(wy) + C_c, C_c = max*(U_c, -U_c) (two max* per step) -- then
+ * max*(a[p0] + pm, a[p0 + 8] + pm') over the two predecessors in table order
+ * (beta: successor classes {0, 3} then {1, 2}).
  * Extrinsic: u[s][c] = alpha[s] + beta[next(s, c)] for the input classes
  * c = {0, 3}, {1, 2}; V[c][wy] = lse4 over the 4 states (in state order) whose
- * class-c branches carry the parity pair wy = 2W + Y; app[inp] = lse4 over wy
- * of (gamma_inp(wy) + V[c(inp)][wy]); LpA = max*(app0, app1) - max*(app2, app3),
+ * class-c branches carry the parity pair wy; X_c = lse4 over wy of
+ * (v(wy) + V[c][wy]); app = {U0 + X_0, U1 + X_1, -U1 + X_1, -U0 + X_0} (inputs
+ * 0..3); LpA = max*(app0, app1) - max*(app2, app3),
  * LpB = max*(app0, app2) - max*(app1, app3) (bits); Le = ((f64)Lp * ln2 - in) * sf
  * clipped to +-300.  That is the log-MAP sum (np.logaddexp over the states)
  * regrouped, so it stays within f32 rounding of log-MAP with exact f64 Jacobian
@@ -207,6 +213,7 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
     float *gamma = (float *)calloc((size_t)N * NS * 4, sizeof(float));
     float *alpha = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
     float *beta = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
+    float *UV = (float *)calloc((size_t)N * 4, sizeof(float));   /* log-MAP: U0, U1, V0, V1 per k */
     const double hw = algo ? LM_K : 0.5;   /* branch-metric half weight: nats (reference) or bits */
 
     /* 1. gamma (:127-160): f64 sum in fixed order, stored as f32 */
@@ -214,6 +221,13 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
         double in_A = (double)LcA[k] + LaA[k];
         double in_B = (double)LcB[k] + LaB[k];
         float par_W = LcW[k], par_Y = LcY[k];
+        if (algo) {   /* log-MAP branch halves (round 4): f64 sums rounded once */
+            const double hA = in_A * hw, hB = in_B * hw, hW = (double)par_W * hw, hY = (double)par_Y * hw;
+            UV[4 * k + 0] = (float)(hA + hB);
+            UV[4 * k + 1] = (float)(hA + (-hB));
+            UV[4 * k + 2] = (float)(hW + hY);
+            UV[4 * k + 3] = (float)(hW + (-hY));
+        }
         for (int s = 0; s < NS; ++s)
             for (int inp = 0; inp < 4; ++inp) {
                 int bA = (inp >> 1) & 1, bB = inp & 1;
@@ -229,6 +243,11 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
 #define GAM(k, s, i) gamma[((size_t)(k) * NS + (s)) * 4 + (i)]
 #define ALP(k, s) alpha[(size_t)(k) * NS + (s)]
 #define BET(k, s) beta[(size_t)(k) * NS + (s)]
+/* log-MAP: v(wy) = {V0, V1, -V1, -V0}; the pair of class c, parity pair wy carries
+ * +-U_c + v(wy), log-sum v(wy) + C_c, C_c = max*(U_c, -U_c) */
+#define LMV(k, wy) ((wy) == 0 ? UV[4 * (k) + 2] : (wy) == 1 ? UV[4 * (k) + 3] : (wy) == 2 ? -UV[4 * (k) + 3] : -UV[4 * (k) + 2])
+#define LMC(k, c) jac(UV[4 * (k) + (c)], -UV[4 * (k) + (c)])
+#define LMPAIR(k, s, inp) (LMV(k, 2 * ow[(s) * 4 + (inp)] + oy[(s) * 4 + (inp)]) + LMC(k, (((inp) >> 1) ^ (inp)) & 1))
 
     /* 2. forward, double pass (:162-197) */
     for (int pass = 0; pass < 2; ++pass) {
@@ -242,9 +261,8 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
                      * predecessors in table order */
                     float t[2];
                     for (int q = 0; q < 2; ++q) {
-                        int idx = 2 * q, p = ps[n * 4 + idx], i0 = pi[n * 4 + idx], i1 = pi[n * 4 + idx + 1];
-                        int lo = i0 < i1 ? i0 : i1, hi = i0 < i1 ? i1 : i0;
-                        t[q] = ALP(k, p) + jac(GAM(k, p, lo), GAM(k, p, hi));
+                        int idx = 2 * q, p = ps[n * 4 + idx], i0 = pi[n * 4 + idx];
+                        t[q] = ALP(k, p) + LMPAIR(k, p, i0);
                     }
                     mv = jac(t[0], t[1]);
                 } else {
@@ -271,8 +289,7 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
                 float mv;
                 if (algo) {
                     /* parallel pairs {0, 3} then {1, 2} (one successor each) */
-                    mv = jac(BET(k + 1, nx[s * 4 + 0]) + jac(GAM(k, s, 0), GAM(k, s, 3)),
-                             BET(k + 1, nx[s * 4 + 1]) + jac(GAM(k, s, 1), GAM(k, s, 2)));
+                    mv = jac(BET(k + 1, nx[s * 4 + 0]) + LMPAIR(k, s, 0), BET(k + 1, nx[s * 4 + 1]) + LMPAIR(k, s, 1));
                 } else {
                     mv = (float)NEG_INF_VAL;
                     for (int inp = 0; inp < 4; ++inp) {
@@ -294,25 +311,20 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
         if (algo) {
             /* classes c = 0 (inputs 0, 3) and 1 (inputs 1, 2): u = alpha + beta(next),
              * grouped by the branches' parity pair wy, then the branch metric per input */
-            float V[2][4];
-            int gs[2][4];   /* a state of each (class, wy) group: its gamma is the group's */
+            float V[2][4], X[2];
             for (int c = 0; c < 2; ++c) {
                 float x[4][4];
                 int cnt[4] = {0, 0, 0, 0};
                 for (int s = 0; s < NS; ++s) {
                     int wy = 2 * ow[s * 4 + c] + oy[s * 4 + c];
-                    if (cnt[wy] == 0) gs[c][wy] = s;
                     x[wy][cnt[wy]++] = ALP(k, s) + BET(k + 1, nx[s * 4 + c]);
                 }
                 for (int wy = 0; wy < 4; ++wy) V[c][wy] = lse4(x[wy][0], x[wy][1], x[wy][2], x[wy][3]);
+                /* the class's two inputs share X_c = lse4 over wy of (v(wy) + V[c][wy]) */
+                X[c] = lse4(LMV(k, 0) + V[c][0], LMV(k, 1) + V[c][1], LMV(k, 2) + V[c][2], LMV(k, 3) + V[c][3]);
             }
-            float app[4];
-            for (int inp = 0; inp < 4; ++inp) {
-                int c = (inp == 1 || inp == 2);
-                float y[4];
-                for (int wy = 0; wy < 4; ++wy) y[wy] = GAM(k, gs[c][wy], inp) + V[c][wy];
-                app[inp] = lse4(y[0], y[1], y[2], y[3]);
-            }
+            const float U0 = UV[4 * k], U1 = UV[4 * k + 1];
+            const float app[4] = {U0 + X[0], U1 + X[1], -U1 + X[1], -U0 + X[0]};
             LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
             LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
         } else {
@@ -344,7 +356,10 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
 #undef GAM
 #undef ALP
 #undef BET
-    free(gamma); free(alpha); free(beta);
+#undef LMV
+#undef LMC
+#undef LMPAIR
+    free(gamma); free(alpha); free(beta); free(UV);
 }
 
 /* ------------------------------------------------------ exact log-MAP -- */

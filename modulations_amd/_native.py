@@ -78,9 +78,12 @@ def _declare(L):
     L.tdec_host_alloc.argtypes = [C.c_size_t, C.POINTER(_vp)]
     L.tdec_host_free.argtypes = [_vp]
     L.tdec_host_free.restype = None
-    L.tdec_encode_host.argtypes = [C.c_int, C.c_int, _vp, _vp, C.c_long, _vp, C.c_long, _vp, C.c_long]
-    L.tdec_encode_host.restype = C.c_long
+    if hasattr(L, "tdec_encode_host"):   # (A/B tools also load older builds without it)
+        L.tdec_encode_host.argtypes = [C.c_int, C.c_int, _vp, _vp, C.c_long, _vp, C.c_long, _vp, C.c_long]
+        L.tdec_encode_host.restype = C.c_long
     for name in EXPORTS:
+        if not hasattr(L, name):
+            continue
         f = getattr(L, name)
         if f.restype is C.c_int or name in ("tdec_siso_batch", "tdec_decode_batch", "tdec_reserve",
                                             "tdec_depuncture_dev", "tdec_decode_planes_dev",

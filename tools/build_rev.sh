@@ -5,8 +5,8 @@ set -euo pipefail
 rev=$1; name=$2; shift 2
 d=$(mktemp -d)
 mkdir -p $d/csrc $d/include
-for f in tdec_api.hip tdec_kernels.hip tdec_workload.hip tdec_spl.hip tdec_lowlat.hip npmath.hip; do
-  git show $rev:modulations_amd/csrc/$f > $d/csrc/$f
+for f in tdec_api.hip tdec_kernels.hip tdec_workload.hip tdec_spl.hip tdec_lowlat.hip tdec_frame.hip npmath.hip; do
+  git show $rev:modulations_amd/csrc/$f > $d/csrc/$f 2>/dev/null || rm -f $d/csrc/$f
 done
 git show $rev:include/tdec.h > $d/include/tdec.h
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \

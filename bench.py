@@ -248,7 +248,7 @@ def host_api(codec, llr_rows, hb, dev):
         ts2.append(time.perf_counter() - t0)
     res["single_call_ms"] = {"decode_752_r12": float(np.median(ts) * 1e3), "decode_min": float(np.min(ts) * 1e3),
                              "bcjr_max_log_map_752": float(np.median(ts2) * 1e3),
-                             "reference_decode_ms": 12.3,
+                             "reference_decode_ms": 12.3, "reference_siso_ms": 0.493,
                              "path": "DVBRCS2_Turbo(752, '1/2').decode(llr) per frame as test.py:81 (median of 20); "
                                      "bcjr_max_log_map(...) at N=752 (median of 20); reference: BASELINE.md §2"}
     return res

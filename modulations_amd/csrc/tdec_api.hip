@@ -333,6 +333,7 @@ struct tdec_ctx {
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
     int32_t *d_used = nullptr;         // [N]: k in the image of perm
     int32_t *d_ulist = nullptr;        // [n_used]: the k in the image of perm, ascending (low-latency decoder)
+    int32_t *d_ford = nullptr;         // [N]: those k, then the others (frame decoder's position order)
     int n_used = 0;
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
@@ -477,6 +478,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     h->n_used = (int)ulist.size();
     if (e == hipSuccess) e = hipMalloc(&h->d_ulist, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMemcpy(h->d_ulist, ulist.data(), sizeof(int32_t) * ulist.size(), hipMemcpyHostToDevice);
+    std::vector<int32_t> ford(ulist);
+    for (int k = 0; k < N; ++k)
+        if (!used[k]) ford.push_back(k);
+    if (e == hipSuccess) e = hipMalloc(&h->d_ford, sizeof(int32_t) * N);
+    if (e == hipSuccess) e = hipMemcpy(h->d_ford, ford.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
@@ -593,6 +599,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_perm);
     hipFree(h->d_used);
     hipFree(h->d_ulist);
+    hipFree(h->d_ford);
     hipFree(h->d_inv);
     hipFree(h->d_src);
     hipFree(h->d_tile_ctr);
@@ -898,7 +905,7 @@ static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // p
 // LDS) takes the small batches when its LDS fits (N <= 790: every BASELINE
 // config); the round-3 state-per-lane decoder (tdec_lowlat.hip) otherwise, or
 // with TDEC_FRAME=0 (A/B).
-static bool frame_fits(int N, bool dec) { return fr_lds(N, dec).total <= FR_LDS_MAX; }
+static bool frame_fits(int N, bool dec) { return N <= FR_J * FR_BLOCK && fr_lds(N, dec).total <= FR_LDS_MAX; }
 static bool use_frame_decoder(const tdec_t *h) {
     const char *e = getenv("TDEC_FRAME");   // read per call: tests switch decoders in-process
     return !(e && e[0] == '0') && frame_fits(h->N, true);
@@ -977,7 +984,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
             if (int rc = frame_lds_attr()) return rc;
             FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used};
             hipLaunchKernelGGL(k_turbo_decode_frame, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true).total, st, a,
-                               (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ulist);
+                               (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ford);
             HIPCHK(hipGetLastError());
             return mark_used(h, st);
         }

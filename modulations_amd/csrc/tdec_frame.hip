@@ -50,12 +50,12 @@ __device__ __forceinline__ void lds_st(lds_b *p, float v) { *(lds_f1 *)p = v; }
 // ---- LDS layout (bytes) ------------------------------------------------------------
 // ev [2][4][16] f32 segment end vectors, sink [2][512 B] (stores of idle groups),
 // st_a [N+1][16] f32 (alpha[k] at row k), st_b [N+1][16] (beta[k] at row k), pmt
-// [N][8] f32 pair maxima; the decoder adds p1, le2 [N] double2 and perm, inv,
-// ulist [N] int.  The recursions read up to 8 rows past pmt / st in either
+// [N][8] f32 pair maxima; the decoder adds p1, le2 [N] double2 and perm, inv
+// [N] int.  The recursions read up to 8 rows past pmt / st in either
 // direction (prefetch; values unused): the arrays before st_a and the tail pad
 // keep those reads inside the allocation.
 struct FrLds {
-    int st_a, st_b, pmt, ev, sink, p1, le2, perm, inv, ulist, total;
+    int st_a, st_b, pmt, ev, sink, p1, le2, perm, inv, total;
 };
 __host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
     FrLds L{};
@@ -65,13 +65,12 @@ __host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
     L.st_a = o; o += (N + 1) * 64;
     L.st_b = o; o += (N + 1) * 64;
     L.pmt = o;  o += N * 32;
-    L.p1 = L.le2 = L.perm = L.inv = L.ulist = o;
+    L.p1 = L.le2 = L.perm = L.inv = o;
     if (dec) {
         L.p1 = o;    o += N * 16;
         L.le2 = o;   o += N * 16;
         L.perm = o;  o += N * 4;
         L.inv = o;   o += N * 4;
-        L.ulist = o; o += N * 4;
     }
     L.total = o + 512;   // tail: the alpha wave's reads past pmt
     return L;
@@ -321,14 +320,20 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 }
 
 // ---- inputs / outputs of one SISO -------------------------------------------------------
-// get(k): the f64 sums inA = f64(Lc_A) + La_A, inB (:135-136), the parities and Lc.
+// Thread t owns the positions ord[t + j * FR_BLOCK] (j < FR_J) in both position-
+// parallel phases of every SISO, so their channel values (In::Raw) are fetched from
+// HBM once per kernel and stay in registers (16 P and 16 E phases per decode: a
+// global-load round trip per phase otherwise).  The decoder's order puts the
+// positions in perm's image first (decoder 1's sparse extrinsic phase is then
+// ord[0 .. n_used)); the SISO kernel's order is the identity.
+constexpr int FR_J = 2;                    // positions per thread: N <= FR_J * FR_BLOCK = 1024
+// get(raw, k): the f64 sums inA = f64(Lc_A) + La_A, inB (:135-136), the parities and Lc.
 struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[k]] (LDS)
-    const float4 *X;
+    typedef float4 Raw;
     const lds_b *le2;
     const lds_int *inv;
-    int cwl;
-    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
-        const float4 x = X[(long)k * WAVE + cwl];
+    __device__ __forceinline__ void get(const Raw &x, int k, double &iA, double &iB, float &w, float &y, float &la,
+                                        float &lb) const {
         const d2v p = *(const lds_d2 *)(le2 + 16 * inv[k]);
         iA = (double)x.x + p.x;
         iB = (double)x.y + p.y;
@@ -339,12 +344,11 @@ struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[
     }
 };
 struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 (LDS; :507-516)
-    const float2 *Z;
+    typedef float2 Raw;
     const lds_b *p1;
     const lds_int *perm;
-    int cwl;
-    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
-        const float2 z = Z[(long)k * WAVE + cwl];
+    __device__ __forceinline__ void get(const Raw &z, int k, double &iA, double &iB, float &w, float &y, float &la,
+                                        float &lb) const {
         const d2v p = *(const lds_d2 *)(p1 + 16 * perm[k]);
         iA = p.x;
         iB = p.y;
@@ -353,27 +357,29 @@ struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 
         la = lb = 0.0f;
     }
 };
+struct FrRowRaw {
+    float a, b, w, y;
+    double la, lb;
+};
 struct FrInRow {   // bcjr_max_log_map's arguments (:116), one row
+    typedef FrRowRaw Raw;
     const float *A, *B, *W, *Y;
     const double *LaA, *LaB;
-    __device__ __forceinline__ void get(int k, double &iA, double &iB, float &w, float &y, float &la, float &lb) const {
-        iA = (double)A[k] + LaA[k];
-        iB = (double)B[k] + LaB[k];
-        w = W[k];
-        y = Y[k];
+    __device__ __forceinline__ Raw fetch(int k) const { return Raw{A[k], B[k], W[k], Y[k], LaA[k], LaB[k]}; }
+    __device__ __forceinline__ void get(const Raw &r, int, double &iA, double &iB, float &w, float &y, float &la,
+                                        float &lb) const {
+        iA = (double)r.a + r.la;
+        iB = (double)r.b + r.lb;
+        w = r.w;
+        y = r.y;
         la = lb = 0.0f;
     }
 };
 struct FrOut1 {  // P1 = f64(Lc) + Le1 for decoder 2 (LDS), Le1 itself in the last iteration (global)
     lds_b *p1;
     double2 *le1;
-    const lds_int *ulist;   // the positions in perm's image (only those are read before the last iteration)
     int n_used;
-    __device__ __forceinline__ bool sparse() const { return !le1; }
-    __device__ __forceinline__ int count(int N) const { return sparse() ? n_used : N; }
-    __device__ __forceinline__ int pos(int i) const {
-        return sparse() ? ulist[i] : i;
-    }
+    __device__ __forceinline__ int count(int N) const { return le1 ? N : n_used; }   // sparse before the last iteration
     __device__ __forceinline__ void store(int k, double a, double b, float la, float lb) const {
         *(lds_d2 *)(p1 + 16 * k) = d2v{(double)la + a, (double)lb + b};
         if (le1) le1[k] = make_double2(a, b);
@@ -382,7 +388,6 @@ struct FrOut1 {  // P1 = f64(Lc) + Le1 for decoder 2 (LDS), Le1 itself in the la
 struct FrOut2 {
     lds_b *le2;
     __device__ __forceinline__ int count(int N) const { return N; }
-    __device__ __forceinline__ int pos(int i) const { return i; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
         *(lds_d2 *)(le2 + 16 * k) = d2v{a, b};
     }
@@ -390,26 +395,30 @@ struct FrOut2 {
 struct FrOutRow {
     double *A, *B;
     __device__ __forceinline__ int count(int N) const { return N; }
-    __device__ __forceinline__ int pos(int i) const { return i; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
         A[k] = a;
         B[k] = b;
     }
 };
 
-// One SISO (:116-281) of the workgroup's codeword.  Ends with a barrier.
+// One SISO (:116-281) of the workgroup's codeword.  pos[j]: this thread's positions
+// (-1: none), raw[j] their channel values.  Ends with a barrier.
 template <class In, class Out>
-__device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo, int N, double sf) {
+__device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], const typename In::Raw (&raw)[FR_J],
+                        lds_b *sm, const FrLds &Lo, int N, double sf) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     lds_b *pmt = sm + Lo.pmt;
 #if TDEC_FR_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     // P: pair maxima of every position
-    for (int k = tid; k < N; k += FR_BLOCK) {
+#pragma unroll
+    for (int j = 0; j < FR_J; ++j) {
+        const int k = pos[j];
+        if (k < 0) continue;
         double iA, iB;
         float w, y, la, lb;
-        in.get(k, iA, iB, w, y, la, lb);
+        in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8], pm[2][4];
         gamma_from_sums(iA, iB, w, y, g);
         pair_max(g, pm);
@@ -428,13 +437,15 @@ __device__ void fr_siso(const In &in, const Out &out, lds_b *sm, const FrLds &Lo
 #if TDEC_FR_STATS
     const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // E: extrinsic of every position anyone reads
+    // E: extrinsic of every position anyone reads (slots i < M of the order)
     const int M = out.count(N);
-    for (int i = tid; i < M; i += FR_BLOCK) {
-        const int k = out.pos(i);
+#pragma unroll
+    for (int j = 0; j < FR_J; ++j) {
+        const int k = pos[j];
+        if (k < 0 || tid + j * FR_BLOCK >= M) continue;
         double iA, iB;
         float w, y, la, lb;
-        in.get(k, iA, iB, w, y, la, lb);
+        in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8];
         gamma_from_sums(iA, iB, w, y, g);
         float a[NS], b[NS];
@@ -470,9 +481,10 @@ struct FrArgs {
 };
 
 // DVBRCS2_Turbo.decode (:464-537) of one codeword per workgroup (grid = B).
+// ord: [N] the positions in perm's image (ascending), then the others.
 __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
                                                                  const int *__restrict__ inv,
-                                                                 const int *__restrict__ ulist) {
+                                                                 const int *__restrict__ ord) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;
     const int N = p.N, tid = threadIdx.x;
@@ -483,11 +495,22 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
     const float *base = p.planes + tile * tile_floats(N);
     const float4 *X = reinterpret_cast<const float4 *>(base);
     const float2 *Z = reinterpret_cast<const float2 *>(base + (long)N * WAVE * 4);
-    lds_int *sperm = (lds_int *)(sm + Lo.perm), *sinv = (lds_int *)(sm + Lo.inv), *sul = (lds_int *)(sm + Lo.ulist);
+    lds_int *sperm = (lds_int *)(sm + Lo.perm), *sinv = (lds_int *)(sm + Lo.inv);
+    // this thread's positions and their planes, once for all 16 SISOs
+    int pos[FR_J];
+    float4 xr[FR_J];
+    float2 zr[FR_J];
+#pragma unroll
+    for (int j = 0; j < FR_J; ++j) {
+        const int i = tid + j * FR_BLOCK;
+        pos[j] = i < N ? ord[i] : -1;
+        const int k = pos[j] < 0 ? 0 : pos[j];
+        xr[j] = X[(long)k * WAVE + cwl];
+        zr[j] = Z[(long)k * WAVE + cwl];
+    }
     for (int k = tid; k < N; k += FR_BLOCK) {
         sperm[k] = perm[k];
         sinv[k] = inv[k];
-        if (k < p.n_used) sul[k] = ulist[k];
         *(lds_d2 *)(sm + Lo.le2 + 16 * k) = d2v{0.0, 0.0};   // the first iteration's a-priori (:490-491)
     }
     __syncthreads();
@@ -495,13 +518,15 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
     for (int it = 0; it < p.iters; ++it) {
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
-        fr_siso(FrIn1{X, sm + Lo.le2, sinv, cwl}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, sul, p.n_used}, sm, Lo, N,
-                sf);
-        fr_siso(FrIn2{Z, sm + Lo.p1, sperm, cwl}, FrOut2{sm + Lo.le2}, sm, Lo, N, sf);
+        fr_siso(FrIn1{sm + Lo.le2, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
+        fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2{sm + Lo.le2}, pos, zr, sm, Lo, N, sf);
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
-    for (int k = tid; k < N; k += FR_BLOCK) {
-        const float4 x = X[(long)k * WAVE + cwl];
+#pragma unroll
+    for (int j = 0; j < FR_J; ++j) {
+        const int k = pos[j];
+        if (k < 0) continue;
+        const float4 x = xr[j];
         const d2v la = *(const lds_d2 *)(sm + Lo.le2 + 16 * sinv[k]);
         const double2 le = le1[k];
         const double fa = ((double)x.x + la.x) + le.x;
@@ -523,8 +548,16 @@ __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;
     const long row = (long)blockIdx.x * p.N;
-    fr_siso(FrInRow{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row},
-            FrOutRow{p.LeA + row, p.LeB + row}, sm, fr_lds(p.N, false), p.N, p.sf);
+    const FrInRow in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
+    int pos[FR_J];
+    FrRowRaw raw[FR_J];
+#pragma unroll
+    for (int j = 0; j < FR_J; ++j) {
+        const int i = threadIdx.x + j * FR_BLOCK;
+        pos[j] = i < p.N ? i : -1;
+        raw[j] = in.fetch(i < p.N ? i : 0);
+    }
+    fr_siso(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
 }
 
 }  // namespace tdec

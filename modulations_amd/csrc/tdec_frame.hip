@@ -139,9 +139,52 @@ template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
 }
 // one trellis step (:165-179 / :203-213 with pair maxima): max over the two branch
 // pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row)
-template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po) {
+// TDEC_FR_N0 (default): every lane also forms state 0's new value itself, from lane
+// 0 and its partner lane 8 >> PH (state 0's two predecessors / successors in both
+// labellings) with state 0's pair maxima pm[0] / pm[7] -- the same operands in
+// the same order as lane 0, so the same bits -- instead of waiting for lane 0's
+// result through a second DPP move: the chain is DPP-add, max3, subtract.
+#ifndef TDEC_FR_N0
+#define TDEC_FR_N0 0
+#endif
+// TDEC_FR_ASM: the partner's add and the normalisation as DPP forms of the VALU
+// ops themselves (v_add_f32_dpp: partner + po; v_subrev_f32_dpp: n - n[lane 0]),
+// not a DPP move feeding them -- 2 fewer instructions on the serial chain (3 in
+// the xor-4 phase).  Same IEEE operations, so the same bits.  The s_nop 1 covers
+// the VALU-write -> DPP-read hazard (2 wait states), which the compiler does not
+// track through inline asm.
+#ifndef TDEC_FR_ASM
+#define TDEC_FR_ASM 1
+#endif
+template <int PH> __device__ __forceinline__ float fr_partner_add(float v, float po) {
+    float y;
+    if constexpr (PH == 0)
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 row_ror:8 row_mask:0xf bank_mask:0xf" : "=v"(y) : "v"(v), "v"(po));
+    else if constexpr (PH == 1)
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+            "v_add_f32_dpp %0, %1, %2 row_shr:4 row_mask:0xf bank_mask:0xa"
+            : "=&v"(y) : "v"(v), "v"(po));
+    else if constexpr (PH == 2)
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf" : "=v"(y) : "v"(v), "v"(po));
+    else
+        asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(y) : "v"(v), "v"(po));
+    return y;
+}
+template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po, float pa, float pb) {
+    if constexpr (TDEC_FR_ASM && !TDEC_FR_N0) {
+        const float y = fr_partner_add<PH>(v, po);
+        const float n = fmaxf(fmaxf(NEG, v + ps), y);
+        float r;
+        asm("s_nop 1\n\tv_subrev_f32_dpp %0, %1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(n));
+        return r;
+    }
     const float o = fr_xchg<PH>(v);
     const float n = fmaxf(fmaxf(NEG, v + ps), o + po);
+    if constexpr (TDEC_FR_N0) {
+        const float v0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150, 0xF, 0xF, false));
+        const float v8 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + (8 >> PH), 0xF, 0xF, false));
+        return n - fmaxf(fmaxf(NEG, v0 + pa), v8 + pb);
+    }
     return n - __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));   // row_newbcast:0
 }
 
@@ -185,7 +228,7 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
     auto prow = [&](int U) { return (DIR ? N - 1 - U : U) * 32; };
     lds_b *const sink_s = R.sink + (DIR ? 256 : 0);
     unsigned long long reached = 0;
-    float pc[4][2], pn[4][2] = {};
+    float pc[4][4], pn[4][4] = {};   // per phase: the lane's own / partner pair maxima, state 0's pm[0] / pm[7]
     float cmpv = 0.0f, cmpn = 0.0f;
     {
         const lds_b *pr = R.pmt + prow(u0);
@@ -193,12 +236,16 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         for (int ph = 0; ph < 4; ++ph) {
             pc[ph][0] = lds_ld(pr + L.poff[ph][0]);
             pc[ph][1] = lds_ld(pr + L.poff[ph][1]);
+            if constexpr (TDEC_FR_N0) {
+                pc[ph][2] = lds_ld(pr + (DIR ? -32 : 32) * ph);
+                pc[ph][3] = lds_ld(pr + (DIR ? -32 : 32) * ph + 28);
+            }
         }
         if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
     }
     // one block of 4 steps from pair maxima `c` while the next block's go to `n`
     // (ping-pong over two register sets: no moves between blocks)
-    auto block = [&](int u, float (&c)[4][2], float (&n)[4][2], float &cv, float &cn) -> bool {
+    auto block = [&](int u, float (&c)[4][4], float (&n)[4][4], float &cv, float &cn) -> bool {
 #if TDEC_FR_STATS
         if (lane == 0) atomicAdd(&g_fr_stats[stat], 1ull);
 #endif
@@ -212,6 +259,10 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
             for (int ph = 0; ph < 4; ++ph) {
                 n[ph][0] = lds_ld(pr + L.poff[ph][0]);
                 n[ph][1] = lds_ld(pr + L.poff[ph][1]);
+                if constexpr (TDEC_FR_N0) {
+                    n[ph][2] = lds_ld(pr + (DIR ? -32 : 32) * ph);
+                    n[ph][3] = lds_ld(pr + (DIR ? -32 : 32) * ph + 28);
+                }
             }
             if constexpr (CMP) cn = lds_ld(R.st + srow(U + 4) + L.soff[0]);
         }
@@ -220,20 +271,20 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
             lds_b *const sr = rl ? srw : sink_s;
             lds_st(sr + L.soff[0], v);
-            v = fr_step<0>(v, c[0][0], c[0][1]);
+            v = fr_step<0>(v, c[0][0], c[0][1], c[0][2], c[0][3]);
             lds_st(sr + L.soff[1], v);
-            v = fr_step<1>(v, c[1][0], c[1][1]);
+            v = fr_step<1>(v, c[1][0], c[1][1], c[1][2], c[1][3]);
             lds_st(sr + L.soff[2], v);
-            v = fr_step<2>(v, c[2][0], c[2][1]);
+            v = fr_step<2>(v, c[2][0], c[2][1], c[2][2], c[2][3]);
             lds_st(sr + L.soff[3], v);
-            v = fr_step<3>(v, c[3][0], c[3][1]);
+            v = fr_step<3>(v, c[3][0], c[3][1], c[3][2], c[3][3]);
         } else {   // some group ends in this block: per-step bounds, end vector captured
             lds_b *const evg = R.ev + g * 64;
 #define FR_SLOW_STEP(PH)                                                       \
     {                                                                          \
         const int uu = u + PH;                                                 \
         if (rl && uu < len) lds_st(srw + L.soff[PH], v);                       \
-        const float vn = fr_step<PH>(v, c[PH][0], c[PH][1]);                   \
+        const float vn = fr_step<PH>(v, c[PH][0], c[PH][1], c[PH][2], c[PH][3]);   \
         if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(PH + 1) & 3], vn);    \
         v = vn;                                                                \
     }

@@ -48,7 +48,7 @@ __device__ __forceinline__ float lds_ld(const lds_b *p) { return *(const lds_f1 
 __device__ __forceinline__ void lds_st(lds_b *p, float v) { *(lds_f1 *)p = v; }
 
 // ---- LDS layout (bytes) ------------------------------------------------------------
-// ev [2][4][16] f32 segment end vectors, sink [2][512 B] (stores of idle groups),
+// ev [2][8][16] f32 segment end vectors (+ 64 B of round control), sink [2][512 B] (stores of idle groups),
 // st_a [N+1][16] f32 (alpha[k] at row k), st_b [N+1][16] (beta[k] at row k), pmt
 // [N][8] f32 pair maxima; the decoder adds p1, le2 [N] double2 and perm, inv
 // [N] int.  The recursions read up to 8 rows past pmt / st in either
@@ -60,7 +60,7 @@ struct FrLds {
 __host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
     FrLds L{};
     int o = 0;
-    L.ev = o;   o += 2 * 4 * 64;
+    L.ev = o;   o += 2 * 8 * 64 + 64;   // 2 directions x 8 segments; + the cross-wave rounds' control words
     L.sink = o; o += 2 * 512;
     L.st_a = o; o += (N + 1) * 64;
     L.st_b = o; o += (N + 1) * 64;
@@ -370,6 +370,130 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     }
 }
 
+// ---- TDEC_FR_WPD 2: 8 segments per direction on two waves each --------------------------
+// The same rounds as fr_recursion, with the segments of one direction spread over
+// two waves (alpha: waves 0-1, beta: waves 2-3), so each round is a workgroup step:
+// every wave (the idle ones too) passes three barriers per round -- starts read
+// before any end vector is written, rounds run, thread 0 advances both
+// directions' round state from the segments that reached their end.
+#ifndef TDEC_FR_WPD
+#define TDEC_FR_WPD 1
+#endif
+struct FrCtl {
+    unsigned dirty[2], reached[2], state[2], broken[2], cmp[2];
+};
+enum { FR_A = 0, FR_FIX1 = 1, FR_FIXN = 2, FR_P2S = 3, FR_P2 = 4 };
+__device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int lane) {
+    volatile __attribute__((address_space(3))) FrCtl *ctl =
+        (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * 8 * 64);
+    const int Ls = (N + 31) / 32 * 4;       // segment length (a multiple of 4)
+    const int nseg = (N + Ls - 1) / Ls;     // 1..8
+    const unsigned all = (1u << nseg) - 1;
+    const bool rw = wave < 4;
+    const int dir = wave >> 1, wl = wave & 1, l = lane & 15, g = lane >> 4, G = 4 * wl + g;
+    const int len = max(0, min(Ls, N - G * Ls)), u0 = len ? G * Ls : 0;
+    if (threadIdx.x == 0)
+        for (int d = 0; d < 2; ++d) {
+            ctl->dirty[d] = all;
+            ctl->reached[d] = 0u;
+            ctl->state[d] = FR_A;
+            ctl->broken[d] = 0u;
+            ctl->cmp[d] = 0u;
+        }
+    FrLane<0> La = fr_lane<0>(l);
+    FrLane<1> Lb = fr_lane<1>(l);
+    const FrRec Ra{sm + Lo.st_a, sm + Lo.pmt, sm + Lo.ev, sm + Lo.sink, N};
+    const FrRec Rb{sm + Lo.st_b, sm + Lo.pmt, sm + Lo.ev + 512, sm + Lo.sink + 512, N};
+    __syncthreads();
+    for (;;) {
+        const unsigned dm = rw ? ctl->dirty[dir] : 0u, cmp = rw ? ctl->cmp[dir] : 0u;
+        const bool any = (ctl->dirty[0] | ctl->dirty[1]) != 0u;
+        unsigned long long run = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if ((dm >> (4 * wl + q)) & 1u) run |= 0xFFFFull << (16 * q);
+        float v = 0.0f;
+        if (rw && cmp) {
+            const int src = G == 0 ? nseg - 1 : G - 1;
+            v = lds_ld((dir ? Rb.ev : Ra.ev) + src * 64 + 4 * (dir ? Lb.lbl[0] : La.lbl[0]));
+        }
+        __syncthreads();   // every start is read before any end vector of this round is written
+        if (!any) break;
+        if (rw && run) {
+            unsigned long long r;
+            const int stat = cmp ? (ctl->state[dir] == FR_P2 || ctl->state[dir] == FR_P2S ? 2 : 1) : 0;
+            if (dir == 0) r = cmp ? fr_round<0, true>(Ra, La, G, lane, u0, len, run, v, stat)
+                                  : fr_round<0, false>(Ra, La, G, lane, u0, len, run, v, stat);
+            else r = cmp ? fr_round<1, true>(Rb, Lb, G, lane, u0, len, run, v, stat)
+                         : fr_round<1, false>(Rb, Lb, G, lane, u0, len, run, v, stat);
+            unsigned bits = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((r >> (16 * q)) & 1ull) bits |= 1u << (4 * wl + q);
+            if (lane == 0 && bits) atomicOr((unsigned *)&ctl->reached[dir], bits);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int d = 0; d < 2; ++d) {
+                const unsigned r = ctl->reached[d];
+                unsigned dirty = 0;
+                switch (ctl->state[d]) {
+                case FR_A: {   // phase A done: re-runs + the speculative second pass on segment 0
+                    const unsigned d1 = (r << 1) & all;
+                    if (d1) {
+                        dirty = d1 | 1u;
+                        ctl->state[d] = FR_FIX1;
+                    } else {
+                        dirty = 1u;
+                        ctl->state[d] = FR_P2S;
+                    }
+                    ctl->cmp[d] = 1u;
+                    break;
+                }
+                case FR_FIX1: {
+                    const unsigned r1 = r & ~1u, dd = (r1 << 1) & all;
+                    const bool spec = !(r1 & (1u << (nseg - 1)));
+                    if (!dd && spec) {
+                        dirty = ((r & 1u) << 1) & all;
+                        ctl->state[d] = FR_P2;
+                    } else {
+                        ctl->broken[d] = r & 1u;
+                        if (dd) {
+                            dirty = dd;
+                            ctl->state[d] = FR_FIXN;
+                        } else {
+                            dirty = 1u;
+                            ctl->state[d] = FR_P2S;
+                        }
+                    }
+                    break;
+                }
+                case FR_FIXN: {
+                    const unsigned dd = (r << 1) & all;
+                    if (dd) {
+                        dirty = dd;
+                    } else {
+                        dirty = 1u;
+                        ctl->state[d] = FR_P2S;
+                    }
+                    break;
+                }
+                case FR_P2S:
+                    dirty = ((r & 1u) || ctl->broken[d]) ? 2u & all : 0u;
+                    ctl->state[d] = FR_P2;
+                    break;
+                default:
+                    dirty = (r << 1) & all;
+                    break;
+                }
+                if (ctl->dirty[d] == 0u) dirty = 0u;   // a finished direction stays finished
+                ctl->dirty[d] = dirty;
+                ctl->reached[d] = 0u;
+            }
+        __syncthreads();
+    }
+}
+
 // ---- inputs / outputs of one SISO -------------------------------------------------------
 // Thread t owns the positions ord[t + j * FR_BLOCK] (j < FR_J) in both position-
 // parallel phases of every SISO, so their channel values (In::Raw) are fetched from
@@ -481,9 +605,13 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
 #if TDEC_FR_STATS
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // R: alpha on wave 0, beta on wave 1
-    if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
-    else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + 256, sm + Lo.sink + 512, N}, lane);
+    // R: alpha on wave 0, beta on wave 1 (TDEC_FR_WPD 2: alpha on waves 0-1, beta on 2-3)
+    if constexpr (TDEC_FR_WPD == 1) {
+        if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
+        else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + 512, sm + Lo.sink + 512, N}, lane);
+    } else {
+        fr_recursion_x(sm, Lo, N, wave, lane);
+    }
     __syncthreads();
 #if TDEC_FR_STATS
     const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();

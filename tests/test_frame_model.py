@@ -104,16 +104,17 @@ def lane_step(v, pm_row, ph, idx):
     return (n - n[0]).astype(np.float32)
 
 
-def frame_recursion(pm, beta):
+def frame_recursion(pm, beta, P=4):
     """The kernel's engine: stored vectors [N][16] in step order (natural state
-    order), after both passes, plus round statistics."""
+    order), after both passes, plus round statistics.  P segments per direction
+    (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2)."""
     N = pm.shape[0]
     lbl, idx = lane_consts(beta)
-    Ls = (N + 15) // 16 * 4
+    Ls = (N + 4 * P - 1) // (4 * P) * 4
     nseg = (N + Ls - 1) // Ls
-    seg = [(g * Ls, max(0, min(Ls, N - g * Ls))) for g in range(4)]
+    seg = [(g * Ls, max(0, min(Ls, N - g * Ls))) for g in range(P)]
     st = np.full((N, 16), np.nan, np.float32)
-    ev = np.zeros((4, 16), np.float32)
+    ev = np.zeros((P, 16), np.float32)
     stats = {"rounds": 0}
 
     def run(g, start_nat, cmp):
@@ -207,10 +208,11 @@ def test_lane_step_equals_serial_step(beta):
 @pytest.mark.parametrize("beta", [False, True])
 @pytest.mark.parametrize("N", [1, 2, 3, 5, 8, 13, 16, 17, 33, 48, 101, 212])
 @pytest.mark.parametrize("scale", [3.0, 1e-3])
-def test_segment_rounds_equal_two_pass(beta, N, scale):
+@pytest.mark.parametrize("P", [4, 8])
+def test_segment_rounds_equal_two_pass(beta, N, scale, P):
     rng = np.random.default_rng(N * 3 + int(beta))
     pm = _pm(rng, N, scale)
-    st, _ = frame_recursion(pm, beta)
+    st, _ = frame_recursion(pm, beta, P)
     np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
 
 
@@ -240,7 +242,7 @@ def test_segment_rounds_random_sweep_covers_every_path():
         if trial % 7 == 0:
             pm[rng.integers(0, N)] = np.nan
         beta = bool(trial % 2)
-        st, stats = frame_recursion(pm, beta)
+        st, stats = frame_recursion(pm, beta, 8 if trial % 4 >= 2 else 4)
         np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
         seen.add((stats["spec"], stats["broken"]))
     assert {(True, False), (False, False), (False, True)} <= seen, seen

@@ -535,6 +535,28 @@ void tdec_destroy(tdec_t *h) {
             const unsigned long long z[8] = {};
             hipMemcpyToSymbol(HIP_SYMBOL(g_pass_cycles), z, sizeof(z));
         }
+        static unsigned long long mh[4][MH_END + 1];
+        if (hipMemcpyFromSymbol(mh, HIP_SYMBOL(g_merge_hist), sizeof(mh)) == hipSuccess) {
+            // merge depth in steps: bucket i = i * 8 steps; "end" = never merged
+            static const char *name[4] = {"F2 lane", "F2 wave", "B2 lane", "B2 wave"};
+            for (int w = 0; w < 4; ++w) {
+                unsigned long long tot = 0, acc = 0;
+                double mean = 0;
+                for (int i = 0; i <= MH_END; ++i) tot += mh[w][i], mean += i < MH_END ? (double)i * 8 * mh[w][i] : 0;
+                if (!tot) continue;
+                fprintf(stderr, "[tdec] merge %s: n %llu mean(merged) %.1f steps", name[w], tot,
+                        mean / std::max(1ull, tot - mh[w][MH_END]));
+                const double q[5] = {0.5, 0.9, 0.99, 0.999, 1.0};
+                int qi = 0;
+                for (int i = 0; i <= MH_END && qi < 5; ++i) {
+                    acc += mh[w][i];
+                    while (qi < 5 && acc >= q[qi] * tot) fprintf(stderr, " p%g %d", q[qi++] * 100, i * 8);
+                }
+                fprintf(stderr, " end %.5f\n", (double)mh[w][MH_END] / tot);
+            }
+            memset(mh, 0, sizeof(mh));
+            hipMemcpyToSymbol(HIP_SYMBOL(g_merge_hist), mh, sizeof(mh));
+        }
     }
 #endif
 #if TDEC_WAVE_TIMING

@@ -843,8 +843,11 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 #endif
 // STORE = false: the recursion alone (log-MAP's F1, whose checkpoints F2 would
 // overwrite almost everywhere: see TDEC_LM_F1_PLAIN).
-template <int ALGO, int W, bool RAG, bool STORE = true, class In>
+// CKI: checkpoint interval when it differs from the group interval W (siso8 with
+// TDEC_CK16: groups of 8 steps, a checkpoint at every other group).
+template <int ALGO, int W, bool RAG, bool STORE = true, int CKI = W, class In>
 __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigned cs, int lane, float (&a)[NS]) {
+    static_assert(CKI % W == 0, "checkpoint interval: a multiple of the group interval");
     // log-MAP: one checkpoint interval per group (its steps are ~10x larger, and
     // the kernel's instruction footprint, not load latency, is what costs)
 #ifndef TDEC_FG_LM
@@ -903,7 +906,8 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
 #pragma unroll
         for (int j = 0; j < FG; ++j) {
             if (tail && k0 + j >= N) continue;
-            if (STORE && j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
+            if (STORE && j % W == 0 && (CKI == W || (k0 + j) % CKI == 0))
+                store_vec<true>(ck, cs, ((k0 + j) / CKI) * 4, lane, a);
             alpha_step<ALGO>(a, g[j]);
         }
     }
@@ -1319,7 +1323,104 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
         window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
-constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16-step grid over the top 256 steps
+// TDEC_CK16 (build variant): alpha checkpoints every 16 steps
+// instead of 8 (half the checkpoint bytes: 64 B per lane per 16 steps written by
+// F1/F2 and read back by B1/B2), the backward sweep still in windows of 8.  The
+// slot then holds alpha[16 floor(k0 / 16)]: an even window (k0 % 16 == 0) reads
+// it as before; an odd one first climbs 8 steps over the NEXT window's inputs
+// (its bottom half staged into sn and its top half loaded into rt at this
+// window's start, so nothing is read twice) to alpha[k0], and the slot keeps
+// alpha[k0 - 8], which is the next window's checkpoint.  alpha[k0] is held in
+// registers across the top half (the register cost TDEC_KEEP_MID measured), the
+// climb waits for loads issued at the window's start, and each odd window does
+// 8 more gammas and alpha steps.  Same f32 / f64 operations: bit-identical.
+#ifndef TDEC_CK16
+#define TDEC_CK16 0
+#endif
+template <int ALGO, bool RAG, class In, class Out>
+__device__ __forceinline__ void back_window16(const In &in, const Out &out, int k0, int len, Raw (&rt)[4],
+                                              const LdsStage &st, const LdsStage &sn,
+                                              float (&b)[NS], const float4 *ck, unsigned cs, int lane, int N,
+                                              double sf) {
+    const int lenT = RAG ? (len > 4 ? len - 4 : 0) : 4;
+    const int lenB = RAG ? (len < 4 ? len : 4) : 4;
+    const int kn = k0 >= 8 ? k0 - 8 : 0;   // the next window
+    const bool odd = (k0 & 8) != 0;       // wave-uniform
+    float gw[4][8], lcA[4], lcB[4];
+    double iAw[4], iBw[4];
+    if (!RAG || lenT > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            in.template gamma<ALGO>(rt[j], gw[j], iAw[j], iBw[j]);
+            lcA[j] = rt[j].v.x;
+            lcB[j] = rt[j].v.y;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
+    float a0[NS];
+    if (odd) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rt[j] = in.load(kn + 4 + j);
+        wait_vm<0>();   // sn (this window's DMA) and rt: the climb reads both now
+        ck_read(st.ck, lane, a0);   // alpha[k0 - 8]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float g[8];
+            double x, y;
+            in.template gamma<ALGO>(in.staged(sn, i), g, x, y);
+            alpha_step<ALGO>(a0, g);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float g[8];
+            double x, y;
+            in.template gamma<ALGO>(rt[i], g, x, y);
+            alpha_step<ALGO>(a0, g);
+        }
+    } else {
+        in.wait_staged();   // st and the slot's DMA have landed (sn may still be in flight)
+        ck_read(st.ck, lane, a0);
+        // the slot's last read has returned before the DMA that overwrites it (back_window8)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ck_stage(ck, cs, (kn / 16) * 4, lane, st.ck);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
+    }
+    if (!RAG || lenT > 0) {
+        float a4[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            a4[s] = a0[s];
+            asm volatile("" : "+v"(a4[s]));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float g[8];
+            double x, y;
+            in.template gamma<ALGO>(in.staged(st, i), g, x, y);
+            alpha_step<ALGO>(a4, g);
+        }
+        window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const Raw r = in.staged(st, j);
+        in.template gamma<ALGO>(r, gw[j], iAw[j], iBw[j]);
+        lcA[j] = r.v.x;
+        lcB[j] = r.v.y;
+    }
+    window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
+}
+
+// beta1 kept at every RSTEP8-th window start: 2 = the same 16-step grid over the
+// top 256 steps as siso<>; 1 (build variant) = an 8-step grid over the top 128
+// steps, so B2 stops up to 8 steps earlier for the same ring writes, but lanes
+// that merge below the top 128 steps run B2 to the end.
+#ifndef TDEC_RSTEP8
+#define TDEC_RSTEP8 2
+#endif
+constexpr int RSTEP8 = TDEC_RSTEP8;
 
 // TDEC_PASS_TIMING (measurement build): per-pass shader-clock cycles summed
 // over all waves (s_memtime, one vector atomic from lane 0 per pass), printed
@@ -1327,15 +1428,26 @@ constexpr int RSTEP8 = 2;   // beta1 kept at every 2nd window start: the same 16
 #ifndef TDEC_PASS_TIMING
 #define TDEC_PASS_TIMING 0
 #endif
+// The same build also histograms where the merge passes end:
+// g_merge_hist[0] F2 per lane, [1] F2 per wave (its deepest lane), in units of
+// 8-step checkpoints from k = 0; [2] B2 per lane, [3] B2 per wave, in 8-step
+// windows from the top.  Bucket MH_END: never merged (ran to the end).
+constexpr int MH_END = 127;
 #if TDEC_PASS_TIMING
 __device__ unsigned long long g_pass_cycles[8];
+__device__ unsigned long long g_merge_hist[4][MH_END + 1];
 __device__ __forceinline__ void pass_mark(unsigned long long &t, int slot) {
     const unsigned long long now = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&g_pass_cycles[slot], now - t);
     t = now;
 }
+__device__ __forceinline__ void merge_mark(int which, int lane_at, int wave_at) {
+    atomicAdd(&g_merge_hist[which][min(lane_at, MH_END)], 1ull);
+    if ((threadIdx.x & (WAVE - 1)) == 0) atomicAdd(&g_merge_hist[which + 1][min(wave_at, MH_END)], 1ull);
+}
 #else
 __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
+__device__ __forceinline__ void merge_mark(int, int, int) {}
 #endif
 
 template <int ALGO, bool RAG, class In, class Out>
@@ -1343,14 +1455,14 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
                       const LdsStage &lb, const LdsStage &lb1, const Prio &pr = Prio{}) {
     unsigned long long tpass = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
     phase_prio(true, pr);
-    constexpr int G = 4, CK = 8;
-    const int top = RAG ? ((N - 1) / CK) * CK : N - CK;
+    constexpr int G = 4, WS = 8, CK = TDEC_CK16 ? 16 : 8;   // window step, checkpoint interval
+    const int top = RAG ? ((N - 1) / WS) * WS : N - WS;
     Raw raw[G];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
     // F1: inputs pipelined one group of FG steps ahead, checkpoint every 8
-    f1_pass<ALGO, CK, RAG>(in, N, ck, cs, lane, a);
+    f1_pass<ALGO, WS, RAG, true, CK>(in, N, ck, cs, lane, a);
     pass_mark(tpass, 0);
     // F2 until merged with F1 at a checkpoint.  (Measured alternative, round 2:
     // the next checkpoint prefetched one interval ahead with unmasked input
@@ -1359,11 +1471,18 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
 #pragma unroll
     for (int j = 0; j < G; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
     bool merged = false;   // per lane, as siso<>
+    int mlane = MH_END, mwave = MH_END;   // TDEC_PASS_TIMING: merge checkpoints
     for (int k0 = 0; k0 < N; k0 += G) {
         const bool at_ck = (k0 & (CK - 1)) == 0;
         if (at_ck) {
-            if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / CK) * 4, lane);
-            if (__all(merged)) break;
+            if (!merged) {
+                merged = lane_equal<true>(a, ck, cs, (k0 / CK) * 4, lane);
+                if (TDEC_PASS_TIMING && merged) mlane = k0 / 8;
+            }
+            if (__all(merged)) {
+                mwave = k0 / 8;
+                break;
+            }
         }
         if (!merged) {
             float g[G][8];
@@ -1383,6 +1502,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         }
     }
     pass_mark(tpass, 1);
+    merge_mark(0, mlane, mwave);
     phase_prio(false, pr);
     // B1 fused with the provisional extrinsic, then B2 until merged (as siso<>)
     float b[NS];
@@ -1410,23 +1530,35 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         }
         ck_stage(ck, cs, (top / CK) * 4, lane, lb.ck);
         merged = false;
-        for (int k0 = top; k0 >= 0; k0 -= CK) {
-            const int r = (top - k0) / CK;
+        mlane = mwave = MH_END;
+        for (int k0 = top; k0 >= 0; k0 -= WS) {
+            const int r = (top - k0) / WS;
             const bool keep = r % RSTEP8 == 0 && r < RING * RSTEP8;
-            if (TDEC_PRIO_FINE && pass == 0 && r == top / (2 * CK)) phase_prio(false, pr, 2);
+            if (TDEC_PRIO_FINE && pass == 0 && r == top / (2 * WS)) phase_prio(false, pr, 2);
             if (pass == 0 && keep) store_vec<false>(ring, cs, r / RSTEP8 * 4, lane, b);   // beta1 entering
             if (pass == 1 && keep) {
-                if (!merged) merged = lane_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane);
-                if (__all(merged)) break;
+                if (!merged) {
+                    merged = lane_equal<false>(b, ring, cs, r / RSTEP8 * 4, lane);
+                    if (TDEC_PASS_TIMING && merged) mlane = r;
+                }
+                if (__all(merged)) {
+                    mwave = r;
+                    break;
+                }
             }
             if (!merged) {
                 const bool odd = r & 1;
-                back_window8<ALGO, RAG>(in, out, k0, RAG ? min(CK, N - k0) : CK, raw, odd ? lb1 : lb,
-                                        odd ? lb : lb1, b, ck, cs, lane, N, sf);
+                if constexpr (TDEC_CK16)
+                    back_window16<ALGO, RAG>(in, out, k0, RAG ? min(WS, N - k0) : WS, raw, odd ? lb1 : lb,
+                                             odd ? lb : lb1, b, ck, cs, lane, N, sf);
+                else
+                    back_window8<ALGO, RAG>(in, out, k0, RAG ? min(WS, N - k0) : WS, raw, odd ? lb1 : lb,
+                                            odd ? lb : lb1, b, ck, cs, lane, N, sf);
             }
         }
         pass_mark(tpass, 2 + pass);
     }
+    merge_mark(2, mlane, mwave);
 }
 
 // ---- kernels --------------------------------------------------------------------

@@ -330,6 +330,7 @@ struct tdec_ctx {
     long llr_len = 0, enc_len = 0;
     int circ[16] = {0};
     int max_waves = 0;                 // resident waves of the decode kernel on this device
+    int n_cu = 0;                      // compute units of the device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
     int32_t *d_used = nullptr;         // [N]: k in the image of perm
     int32_t *d_ulist = nullptr;        // [n_used]: the k in the image of perm, ascending (low-latency decoder)
@@ -420,8 +421,13 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
         if (perm[k] < 0 || perm[k] >= n_couples || inv_perm[k] < 0 || inv_perm[k] >= n_couples)
             return fail(TDEC_EINVAL, "perm / inv_perm entry out of range");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
-        return fail(TDEC_EHIP, "no such HIP device");
+    const hipError_t dc = hipGetDeviceCount(&ndev);
+    if (dc != hipSuccess || device < 0 || device >= ndev) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "no such HIP device (device %d, hipGetDeviceCount: %d devices, %s)", device, ndev,
+                 hipGetErrorString(dc));
+        return fail(TDEC_EHIP, msg);
+    }
     Guard g(device);
     auto *h = new tdec_ctx;
     h->device = device;
@@ -504,6 +510,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
         return fail(TDEC_EHIP, std::string("tdec_create: ") + hipGetErrorString(e));
     }
     h->max_waves = std::max(1, blocks_per_cu) * n_cu * DEC_WAVES;
+    h->n_cu = n_cu;
     if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
@@ -1397,19 +1404,31 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep};
     const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
     const int chunks = (h->N + DM_KC - 1) / DM_KC;
-    const dim3 grid((unsigned)((long)n_tiles_of(B) * chunks));
+    const long n_items = (long)n_tiles_of(B) * chunks;   // (64-codeword tile, 16-couple chunk) pairs
     float *P = d_planes;
+    // TDEC_DM_PERSIST: one round of resident blocks (occupancy of this instance)
+    static int bpc_cache[2][9];
+    auto grid_of = [&](const void *kern, int f64) {
+        int &bpc = bpc_cache[f64][bps];
+        if (TDEC_DM_PERSIST && bpc == 0 &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, BLOCK, 0) != hipSuccess)
+            bpc = -1;
+        const long resident = TDEC_DM_PERSIST && bpc > 0 ? (long)bpc * std::max(1, h->n_cu) : n_items;
+        return dim3((unsigned)std::min(n_items, resident));
+    };
     switch (bps) {
 #define CASE(K)                                                                                              \
     case K:                                                                                                  \
         if (cons_f64)                                                                                        \
-            hipLaunchKernelGGL((k_demap_planes<double, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,     \
+            hipLaunchKernelGGL((k_demap_planes<double, K>), grid_of((const void *)k_demap_planes<double, K>, 1),   \
+                               dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
                                (const double *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off, \
-                               n_avail, P);                                                                  \
+                               n_avail, P, n_items);                                                         \
         else                                                                                                 \
-            hipLaunchKernelGGL((k_demap_planes<float, K>), grid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,      \
+            hipLaunchKernelGGL((k_demap_planes<float, K>), grid_of((const void *)k_demap_planes<float, K>, 0),     \
+                               dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
                                (const float *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off,  \
-                               n_avail, P);                                                                  \
+                               n_avail, P, n_items);                                                         \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE

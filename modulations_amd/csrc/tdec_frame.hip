@@ -139,11 +139,13 @@ template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
 }
 // one trellis step (:165-179 / :203-213 with pair maxima): max over the two branch
 // pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row)
-// TDEC_FR_N0 (default): every lane also forms state 0's new value itself, from lane
+// TDEC_FR_N0 (build variant): every lane also forms state 0's new value itself, from lane
 // 0 and its partner lane 8 >> PH (state 0's two predecessors / successors in both
 // labellings) with state 0's pair maxima pm[0] / pm[7] -- the same operands in
 // the same order as lane 0, so the same bits -- instead of waiting for lane 0's
 // result through a second DPP move: the chain is DPP-add, max3, subtract.
+// Measured slower (profiles/r04e/ab_frame_*: 0.39 vs 0.34 ms per decode at B = 1,
+// 1.70 vs 1.50 ms at B = 1 024): the extra VALU work outweighs the shorter chain.
 #ifndef TDEC_FR_N0
 #define TDEC_FR_N0 0
 #endif
@@ -152,7 +154,8 @@ template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
 // not a DPP move feeding them -- 2 fewer instructions on the serial chain (3 in
 // the xor-4 phase).  Same IEEE operations, so the same bits.  The s_nop 1 covers
 // the VALU-write -> DPP-read hazard (2 wait states), which the compiler does not
-// track through inline asm.
+// track through inline asm.  Measured 0.34 vs 0.35 ms per decode at B = 1, 1.50
+// vs 1.52 ms at B = 1 024 (profiles/r04e/ab_frame_*).
 #ifndef TDEC_FR_ASM
 #define TDEC_FR_ASM 1
 #endif
@@ -376,8 +379,10 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 // every wave (the idle ones too) passes three barriers per round -- starts read
 // before any end vector is written, rounds run, thread 0 advances both
 // directions' round state from the segments that reached their end.
+// Measured (profiles/r04e/ab_frame_*, decode of N = 752 r = 1/2): 0.30 vs 0.34 ms
+// at B = 1, 0.36 vs 0.38 ms at B = 64, 1.40 vs 1.50 ms at B = 1 024: the default.
 #ifndef TDEC_FR_WPD
-#define TDEC_FR_WPD 1
+#define TDEC_FR_WPD 2
 #endif
 struct FrCtl {
     unsigned dirty[2], reached[2], state[2], broken[2], cmp[2];

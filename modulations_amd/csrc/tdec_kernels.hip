@@ -2390,8 +2390,8 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 }
 
 // Fused demap -> f32 -> de-puncture planes (the bench path).
-// One block = one 64-codeword tile x DM_KC trellis steps.  Phase 1: the
-// block's threads demap every symbol covering the LLR range of those steps
+// One item = one 64-codeword tile x DM_KC trellis steps (a block loops over
+// items, TDEC_DM_BPC).  Phase 1: the block's threads demap every symbol covering the LLR range of those steps
 // (couples consume LLRs in order, so the range is contiguous) into an LDS
 // tile [64 codewords][range], decoder sign, rounded to f32 as decode() does
 // (:466).  Phase 2: each thread assembles whole plane entries
@@ -2400,105 +2400,132 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 // (:469-474; the harness pads to n_coded, test_sdr_with_coding.py:474-478).
 // src[c*N + k] = LLR index of plane component c (X.xyzw, -, -, Z.xy) or -1;
 // off[k] = first LLR index of couple k (off[N] = n_llr).
+// TDEC_DM_LEAN (round 4, square 16 / 64 / 256QAM): phase 1 runs only the fast
+// exact search (per-axis / Gray positions) and queues the symbols it declines
+// (near ties, non-finite, a non-separable table) in a compact LDS list; a second
+// loop gives those, densely packed, the rest of demap_sym's chain (the
+// sequential per-axis search, then the exact scan).  Inline in one loop, the
+// fallbacks' registers are the kernel's (256QAM: 142 VGPRs and 289 spilled
+// SGPRs against 89 for the Gray search alone).  Same planes: every path returns
+// the scan's LLRs.  Measured (profiles/r04e/ab_demap_*): the first form, a
+// bitmask and the full scan for every declined symbol, lane-sparse, was 2.3x
+// slower on 256QAM; off by default until the A/B says otherwise.
 #ifndef TDEC_DM_LEAN
-#define TDEC_DM_LEAN 1
+#define TDEC_DM_LEAN 0
+#endif
+// TDEC_DM_PERSIST: k_demap_planes' grid is the device's resident blocks (each
+// looping over (tile, chunk) items with its table loaded once) instead of one
+// block per item.  An item is 64 codewords x 16 couples; its table upload
+// (256QAM: 708 entries) and two barriers cost as much as its 768 symbols.
+#ifndef TDEC_DM_PERSIST
+#define TDEC_DM_PERSIST 1
 #endif
 constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
 
+// demap_sym after the fast search declined (lean phase 2)
+template <typename T, int BPS>
+__device__ __forceinline__ void demap_fallback(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    if constexpr (BPS >= 8 && BPS % 2 == 0) {
+        if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return;
+    } else if constexpr (BPS >= 6 && BPS % 2 == 0) {
+        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return;
+    }
+    sym_llrs<T, BPS>(sr, si, cons, c, out);
+}
+
 template <typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *__restrict__ src,
-                                                       const int *__restrict__ off, long n_avail, float *planes) {
+                                                       const int *__restrict__ off, long n_avail, float *planes,
+                                                       long n_items) {
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
-    // TDEC_DM_LEAN (round 4, square 16 / 64 / 256QAM): phase 1 runs only the fast
-    // exact search (per-axis / Gray positions) and queues the symbols it declines
-    // (near ties, non-finite, a non-separable table); a second loop gives those
-    // the exact scan.  Inline in one loop, the fallback's registers were the
-    // kernel's (256QAM: 142 VGPRs and 289 spilled SGPRs against 88 and none for
-    // the Gray search alone).  Same planes: every path returns the scan's LLRs.
     constexpr bool LEAN = TDEC_DM_LEAN && BPS >= 4 && BPS % 2 == 0;
-    constexpr int QW = LEAN ? (WAVE * (DM_MAXL / BPS + 2) + 31) / 32 : 1;   // bitmask words over the items
-    __shared__ unsigned fq[QW];
-    if constexpr (LEAN)
-        for (int i = threadIdx.x; i < QW; i += BLOCK) fq[i] = 0u;
+    constexpr int QN = LEAN ? WAVE * (DM_MAXL / BPS + 2) : 1;   // max items of a block
+    __shared__ unsigned short fl[QN];
+    __shared__ int fn;
+    if (LEAN && threadIdx.x == 0) fn = 0;
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + DM_KC - 1) / DM_KC;
-    const long tile = blockIdx.x / chunks;
-    const int k0 = (int)(blockIdx.x % chunks) * DM_KC;
-    const int k1 = min(N, k0 + DM_KC);
-    const long j0 = off[k0], j1 = off[k1];
-    const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
-    const int ns = (int)(s1 - s0);
     __syncthreads();
-    // item t = (lane, si), consecutive threads: consecutive symbols; the
-    // quotient and remainder of t by ns advance by those of BLOCK each step
-    const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
-    int lane = (int)threadIdx.x / ns, si = (int)threadIdx.x - lane * ns;
-    for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK, lane += dq, si += dr) {
-        if (si >= ns) {
-            si -= ns;
-            ++lane;
-        }
-        const long cw = tile * WAVE + lane;
-        const long s = s0 + si;
-        if (cw >= B || s >= S) continue;
-        const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
-        double v[BPS];
-        if constexpr (LEAN) {
-            // the fast exact search: Gray positions (64 / 256QAM) or the per-axis search (16QAM)
-            bool ok;
-            if constexpr (BPS >= 6) ok = c.sep == 2 && sym_llrs_gray<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-            else ok = c.sep && sym_llrs_sep<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-            if (!ok) {
-                const int it = lane * ns + si;   // < QW * 32
-                atomicOr(&fq[it >> 5], 1u << (it & 31));
-                continue;
+    for (long item = blockIdx.x; item < n_items; item += gridDim.x) {
+        const long tile = item / chunks;
+        const int k0 = (int)(item % chunks) * DM_KC;
+        const int k1 = min(N, k0 + DM_KC);
+        const long j0 = off[k0], j1 = off[k1];
+        const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
+        const int ns = (int)(s1 - s0);
+        // item t = (lane, si), consecutive threads: consecutive symbols; the
+        // quotient and remainder of t by ns advance by those of BLOCK each step
+        const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
+        int lane = (int)threadIdx.x / ns, si = (int)threadIdx.x - lane * ns;
+        for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK, lane += dq, si += dr) {
+            if (si >= ns) {
+                si -= ns;
+                ++lane;
             }
-        } else {
-            demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-        }
-#pragma unroll
-        for (int b = 0; b < BPS; ++b) {
-            const long j = s * BPS + b;
-            if (j >= j0 && j < j1) L[lane * DM_LD + (int)(j - j0)] = (float)v[b];
-        }
-    }
-    __syncthreads();
-    if constexpr (LEAN) {
-        for (int it = threadIdx.x; it < WAVE * ns; it += BLOCK) {
-            if (!((fq[it >> 5] >> (it & 31)) & 1u)) continue;
-            const int ln = it / ns, sx = it - ln * ns;
-            const long cw = tile * WAVE + ln, s = s0 + sx;
+            const long cw = tile * WAVE + lane;
+            const long s = s0 + si;
+            if (cw >= B || s >= S) continue;
             const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
             double v[BPS];
-            sym_llrs_scan<T, BPS, false, (1 << BPS), (BPS <= 4 ? 16 : 1)>((T)z.x, (T)z.y, cons, c, v);
+            if constexpr (LEAN) {
+                // the fast exact search: Gray positions (64 / 256QAM) or the per-axis search (16QAM)
+                bool ok;
+                if constexpr (BPS >= 6) ok = c.sep == 2 && sym_llrs_gray<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+                else ok = c.sep && sym_llrs_sep<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+                if (!ok) {
+                    fl[atomicAdd(&fn, 1)] = (unsigned short)(lane * ns + si);   // < QN
+                    continue;
+                }
+            } else {
+                demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+            }
 #pragma unroll
             for (int b = 0; b < BPS; ++b) {
                 const long j = s * BPS + b;
-                if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
+                if (j >= j0 && j < j1) L[lane * DM_LD + (int)(j - j0)] = (float)v[b];
             }
         }
         __syncthreads();
-    }
-    float *base = planes + tile * tile_floats(N);
-    for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
-        const int lane = t & (WAVE - 1);
-        const int q = __builtin_amdgcn_readfirstlane(t >> 6);   // (step, half): wave-uniform, so src[] is read by scalar loads
-        const int k = k0 + q / 2, half = q & 1;
-        const long cw = tile * WAVE + lane;
-        const int nc = half ? 2 : 4;
-        float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (LEAN) {
+            const int nq = fn;
+            for (int q = threadIdx.x; q < nq; q += BLOCK) {
+                const int it = fl[q];
+                const int ln = it / ns, sx = it - ln * ns;
+                const long cw = tile * WAVE + ln, s = s0 + sx;
+                const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+                double v[BPS];
+                demap_fallback<T, BPS>((T)z.x, (T)z.y, cons, c, v);
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-            if (cc >= nc) break;
-            const int j = src[(long)(half ? 6 + cc : cc) * N + k];
-            v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * DM_LD + (int)(j - j0)] : 0.0f;
+                for (int b = 0; b < BPS; ++b) {
+                    const long j = s * BPS + b;
+                    if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) fn = 0;   // ordered before the next item's queueing by the barrier below
         }
-        if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
-        else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
+        float *base = planes + tile * tile_floats(N);
+        for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
+            const int lane = t & (WAVE - 1);
+            const int q = __builtin_amdgcn_readfirstlane(t >> 6);   // (step, half): wave-uniform, so src[] is read by scalar loads
+            const int k = k0 + q / 2, half = q & 1;
+            const long cw = tile * WAVE + lane;
+            const int nc = half ? 2 : 4;
+            float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                if (cc >= nc) break;
+                const int j = src[(long)(half ? 6 + cc : cc) * N + k];
+                v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * DM_LD + (int)(j - j0)] : 0.0f;
+            }
+            if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+            else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
+        }
+        __syncthreads();   // L (and the lean list) are rewritten by the next item
     }
 }
 

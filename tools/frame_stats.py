@@ -13,6 +13,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["TDEC_LIB_VARIANT"] = "frstats"
+import torch  # noqa: E402,F401  (the HIP runtime torch loads: see tools/hip_probe.py)
 from modulations_amd import _native as _n  # noqa: E402
 from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402
 

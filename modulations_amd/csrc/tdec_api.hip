@@ -1200,6 +1200,18 @@ int tdec_frame_stats(unsigned long long *out) {
 }
 #endif
 
+#if TDEC_DM_STATS
+// measurement build only: symbols per demap path since the last call (see dm_count)
+int tdec_demap_stats(unsigned long long *out) {
+    hipDeviceSynchronize();
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dm_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(TDEC_EHIP, "g_dm_stats");
+    const unsigned long long z[8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_dm_stats), z, sizeof(z));
+    return 0;
+}
+#endif
+
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
                     const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {
     if (!h || B < 0) return fail(TDEC_EINVAL, "bad siso arguments");

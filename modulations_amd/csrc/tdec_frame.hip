@@ -137,6 +137,16 @@ template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
     if constexpr (PH == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
     return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false));                           // quad_perm [1,0,3,2]
 }
+// TDEC_FR_UNI: the round's lane mask in SGPRs (uni64)
+#ifndef TDEC_FR_UNI
+#define TDEC_FR_UNI 1
+#endif
+// TDEC_FR_EXP (timing experiments only, WRONG RESULTS): 1 = no vector stores in the
+// fast blocks, 2 = no pair-maxima loads for the next block, 4 = no step (the
+// vector passes through)
+#ifndef TDEC_FR_EXP
+#define TDEC_FR_EXP 0
+#endif
 // one trellis step (:165-179 / :203-213 with pair maxima): max over the two branch
 // pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row)
 // TDEC_FR_N0 (build variant): every lane also forms state 0's new value itself, from lane
@@ -174,6 +184,7 @@ template <int PH> __device__ __forceinline__ float fr_partner_add(float v, float
     return y;
 }
 template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po, float pa, float pb) {
+    if constexpr ((TDEC_FR_EXP & 4) != 0) return v + ps;
     if constexpr (TDEC_FR_ASM && !TDEC_FR_N0) {
         const float y = fr_partner_add<PH>(v, po);
         const float n = fmaxf(fmaxf(NEG, v + ps), y);
@@ -192,6 +203,14 @@ template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, fl
 }
 
 // lanes of the 16-lane groups whose 16 bits of m are all set
+// A wave-uniform 64-bit value the compiler cannot prove uniform (it came from LDS or
+// a lane-dependent expression), moved to SGPRs: the round loop's control flow
+// then stays scalar (branches on SCC) instead of divergent exec-mask loops with
+// the masks held in VGPRs.
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
 __device__ __forceinline__ unsigned long long grp_all16(unsigned long long m) {
     unsigned long long r = 0;
 #pragma unroll
@@ -208,6 +227,8 @@ struct FrRec {
     int N;
 };
 
+// TDEC_FR_STATS (measurement builds): 1 = block / round counters and phase timers,
+// 2 = the phase timers alone (no atomics inside the recursion loops)
 #ifndef TDEC_FR_STATS
 #define TDEC_FR_STATS 0
 #endif
@@ -226,6 +247,7 @@ template <int DIR, bool CMP>
 __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrLane<DIR> &L, int g, int lane, int u0,
                                                        int len, unsigned long long run, float v, int stat) {
     const int N = R.N;
+    if (TDEC_FR_UNI) run = uni64(run);
     // byte offsets of the rows of step U: store row (alpha[U] / beta[N - U]) and pm row (position)
     auto srow = [&](int U) { return (DIR ? N - U : U) * 64; };
     auto prow = [&](int U) { return (DIR ? N - 1 - U : U) * 32; };
@@ -249,14 +271,14 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
     // one block of 4 steps from pair maxima `c` while the next block's go to `n`
     // (ping-pong over two register sets: no moves between blocks)
     auto block = [&](int u, float (&c)[4][4], float (&n)[4][4], float &cv, float &cn) -> bool {
-#if TDEC_FR_STATS
+#if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[stat], 1ull);
 #endif
         if constexpr (CMP) run &= ~grp_all16(__ballot(v == cv));   // merged: the rest is stored already
         if (!run) return false;
         const int U = u0 + u;
         // the next block's pair maxima and compare value (rows past the end are read, unused)
-        {
+        if (!(TDEC_FR_EXP & 2)) {
             const lds_b *pr = R.pmt + prow(U + 4);
 #pragma unroll
             for (int ph = 0; ph < 4; ++ph) {
@@ -273,13 +295,13 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         lds_b *const srw = R.st + srow(U);
         if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
             lds_b *const sr = rl ? srw : sink_s;
-            lds_st(sr + L.soff[0], v);
+            if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[0], v);
             v = fr_step<0>(v, c[0][0], c[0][1], c[0][2], c[0][3]);
-            lds_st(sr + L.soff[1], v);
+            if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[1], v);
             v = fr_step<1>(v, c[1][0], c[1][1], c[1][2], c[1][3]);
-            lds_st(sr + L.soff[2], v);
+            if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[2], v);
             v = fr_step<2>(v, c[2][0], c[2][1], c[2][2], c[2][3]);
-            lds_st(sr + L.soff[3], v);
+            if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[3], v);
             v = fr_step<3>(v, c[3][0], c[3][1], c[3][2], c[3][3]);
         } else {   // some group ends in this block: per-step bounds, end vector captured
             lds_b *const evg = R.ev + g * 64;
@@ -330,7 +352,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     const unsigned long long G0 = 0xFFFFull, GL = 0xFFFFull << (16 * (nseg - 1));
     bool spec = false, broken = false;
     if (dirty) {
-#if TDEC_FR_STATS
+#if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
         reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty | G0, lds_ld(src), 1);
@@ -348,7 +370,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
         }
         // the remaining pass-1 rounds
         while (!spec && dirty) {
-#if TDEC_FR_STATS
+#if TDEC_FR_STATS == 1
             if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
             reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
@@ -358,14 +380,14 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     // the second pass (from alpha1[N] / beta1[0] at segment 0) unless the
     // speculative start was right, then its remaining rounds
     if (!spec) {
-#if TDEC_FR_STATS
+#if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
         reached = fr_round<DIR, true>(R, L, g, lane, u0, len, G0, lds_ld(src), 2);
         dirty = ((reached & G0) || broken) ? (G0 << 16) & all : 0ull;
     }
     while (dirty) {
-#if TDEC_FR_STATS
+#if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
         reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 2);
@@ -410,6 +432,12 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
     const FrRec Ra{sm + Lo.st_a, sm + Lo.pmt, sm + Lo.ev, sm + Lo.sink, N};
     const FrRec Rb{sm + Lo.st_b, sm + Lo.pmt, sm + Lo.ev + 512, sm + Lo.sink + 512, N};
     __syncthreads();
+#if TDEC_FR_STATS == 2
+    // timers-only build: [0] ticks of round 0 (phase A), [1] of the later rounds,
+    // [2] rounds, [3] ticks wave 0 spends inside fr_round, [4] ticks of wave 0's phase A
+    unsigned long long t_round = __builtin_amdgcn_s_memrealtime();
+    int n_round = 0;
+#endif
     for (;;) {
         const unsigned dm = rw ? ctl->dirty[dir] : 0u, cmp = rw ? ctl->cmp[dir] : 0u;
         const bool any = (ctl->dirty[0] | ctl->dirty[1]) != 0u;
@@ -425,6 +453,9 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
         __syncthreads();   // every start is read before any end vector of this round is written
         if (!any) break;
         if (rw && run) {
+#if TDEC_FR_STATS == 2
+            const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
+#endif
             unsigned long long r;
             const int stat = cmp ? (ctl->state[dir] == FR_P2 || ctl->state[dir] == FR_P2S ? 2 : 1) : 0;
             if (dir == 0) r = cmp ? fr_round<0, true>(Ra, La, G, lane, u0, len, run, v, stat)
@@ -436,6 +467,13 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
             for (int q = 0; q < 4; ++q)
                 if ((r >> (16 * q)) & 1ull) bits |= 1u << (4 * wl + q);
             if (lane == 0 && bits) atomicOr((unsigned *)&ctl->reached[dir], bits);
+#if TDEC_FR_STATS == 2
+            if (threadIdx.x == 0) {
+                const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - tw;
+                atomicAdd(&g_fr_stats[3], dt);
+                if (n_round == 0) atomicAdd(&g_fr_stats[4], dt);
+            }
+#endif
         }
         __syncthreads();
         if (threadIdx.x == 0)
@@ -496,6 +534,15 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
                 ctl->reached[d] = 0u;
             }
         __syncthreads();
+#if TDEC_FR_STATS == 2
+        if (threadIdx.x == 0) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&g_fr_stats[n_round == 0 ? 0 : 1], now - t_round);
+            atomicAdd(&g_fr_stats[2], 1ull);
+            t_round = now;
+        }
+        ++n_round;
+#endif
     }
 }
 

@@ -2290,6 +2290,23 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
     return true;
 }
 
+// TDEC_DM_STATS (measurement build): symbols per demap path, read by
+// tdec_demap_stats: [0] symbols, [1] taken by the Gray search, [2] by the
+// per-axis searches, [3] by the full scan, [4] the table's sep class of the last
+// symbol (+1)
+#ifndef TDEC_DM_STATS
+#define TDEC_DM_STATS 0
+#endif
+#if TDEC_DM_STATS
+__device__ unsigned long long g_dm_stats[8];
+__device__ __forceinline__ void dm_count(int path, int sep) {
+    atomicAdd(&g_dm_stats[0], 1ull);
+    atomicAdd(&g_dm_stats[path], 1ull);
+    g_dm_stats[4] = (unsigned long long)(sep + 1);
+}
+#else
+__device__ __forceinline__ void dm_count(int, int) {}
+#endif
 template <typename T, int BPS>
 __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
 #ifndef TDEC_DM_GRAY
@@ -2298,14 +2315,15 @@ __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const Demap
     // 64 / 256QAM (measured, 1 M codewords, same planes: 20.2 -> 17.6 ms, 70.3 -> 56.2 ms);
     // 16QAM's 4-level scan is cheaper than the table lookups (14.9 vs 16.0 ms)
     if constexpr (TDEC_DM_GRAY && BPS >= 6 && BPS % 2 == 0) {
-        if (c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out)) return;
+        if (c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out)) return dm_count(1, c.sep);
     }
     if constexpr (BPS >= 8 && BPS % 2 == 0) {
-        if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return;
+        if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return dm_count(2, c.sep);
     } else if constexpr (BPS >= 4 && BPS % 2 == 0) {
-        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return;
+        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return dm_count(2, c.sep);
     }
     sym_llrs<T, BPS>(sr, si, cons, c, out);
+    dm_count(3, c.sep);
 }
 
 // The table (and a separable table's axis levels) into LDS.
@@ -2413,12 +2431,13 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_LEAN
 #define TDEC_DM_LEAN 0
 #endif
-// TDEC_DM_PERSIST: k_demap_planes' grid is the device's resident blocks (each
-// looping over (tile, chunk) items with its table loaded once) instead of one
-// block per item.  An item is 64 codewords x 16 couples; its table upload
-// (256QAM: 708 entries) and two barriers cost as much as its 768 symbols.
+// TDEC_DM_PERSIST (build variant): k_demap_planes' grid is the device's resident
+// blocks, each looping over (tile, chunk) items with its table loaded once,
+// instead of one block per item.  Measured slower on every table
+// (profiles/r04f/ab_demap_*: 256QAM 59.0 vs 57.0 ms, 16QAM 19.3 vs 16.9 ms per
+// 1 M codewords): the table upload is not what the kernel waits on.
 #ifndef TDEC_DM_PERSIST
-#define TDEC_DM_PERSIST 1
+#define TDEC_DM_PERSIST 0
 #endif
 constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)

@@ -63,6 +63,20 @@ def main():
     for p, t, pl in zip(a.libs, times, planes):
         print(f"{os.path.basename(p):24s} k_demap_planes median {np.median(t):7.3f} ms  min {np.min(t):7.3f}  "
               f"same_planes={torch.equal(pl, planes[0])}")
+    # measurement builds (TDEC_DM_STATS=1): symbols per path over one more launch
+    for p, L, h, pl in zip(a.libs, libs, hs, planes):
+        try:
+            fn = L.tdec_demap_stats
+        except AttributeError:
+            continue
+        out = (C.c_ulonglong * 8)()
+        fn(out)
+        assert L.tdec_demap_planes_dev(h, B, syms.data_ptr(), syms.shape[1], cons.ctypes.data, 0, len(cons), bps,
+                                       float(nve), int(div32), pl.data_ptr(), st.cuda_stream) == 0
+        fn(out)
+        n = max(1, out[0])
+        print(f"{os.path.basename(p):24s} paths: symbols {out[0]}  gray {out[1] / n:.5f}  per-axis {out[2] / n:.5f}  "
+              f"scan {out[3] / n:.5f}  sep class {int(out[4]) - 1}  div_f32 {int(div32)}")
     for L, h in zip(libs, hs):
         L.tdec_destroy(h)
 

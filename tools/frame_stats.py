@@ -12,7 +12,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["TDEC_LIB_VARIANT"] = "frstats"
+os.environ["TDEC_LIB_VARIANT"] = os.environ.get("FRSTATS_VARIANT", "frstats")   # frtime: TDEC_FR_STATS=2
 import torch  # noqa: E402,F401  (the HIP runtime torch loads: see tools/hip_probe.py)
 from modulations_amd import _native as _n  # noqa: E402
 from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402
@@ -43,6 +43,13 @@ def main():
                                   "pass2": 4 * out[2] / sisos},
            "rounds_per_siso_dir": {"fixup": out[3] / sisos, "pass2": out[4] / sisos},
            "us_per_siso": {ph: round(out[i] * 0.01 / (sisos // 2), 3) for i, ph in ((5, "P"), (6, "R"), (7, "E"))}}
+    if os.environ["TDEC_LIB_VARIANT"] != "frstats":   # timers-only build (TDEC_FR_STATS=2, two waves per direction)
+        res = {"N": n, "rate": rate, "ebn0": ebn0, "B": B,
+               "us_per_siso": res["us_per_siso"],
+               "rounds_per_siso": out[2] / (sisos // 2),
+               "us_per_siso_R": {"round0_phaseA": out[0] * 0.01 / (sisos // 2), "later_rounds": out[1] * 0.01 / (sisos // 2),
+                                 "wave0_in_fr_round": out[3] * 0.01 / (sisos // 2),
+                                 "wave0_phaseA": out[4] * 0.01 / (sisos // 2)}}
     print(json.dumps(res))
 
 

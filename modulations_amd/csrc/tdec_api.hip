@@ -332,6 +332,12 @@ struct tdec_ctx {
     int max_waves = 0;                 // resident waves of the decode kernel on this device
     int n_cu = 0;                      // compute units of the device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
+    int32_t *d_dst = nullptr;          // LLR index -> c * N + k of the plane component it feeds (-1: none)
+    // k_demap_planes' decline list (TDEC_DM_SPLIT): entries, count, per-tile overflow flags
+    int2 *d_decl = nullptr;
+    unsigned *d_decl_n = nullptr;
+    unsigned char *d_decl_ovf = nullptr;
+    long decl_tiles = 0;
     int32_t *d_used = nullptr;         // [N]: k in the image of perm
     int32_t *d_ulist = nullptr;        // [n_used]: the k in the image of perm, ascending (low-latency decoder)
     int32_t *d_ford = nullptr;         // [N]: those k, then the others (frame decoder's position order)
@@ -491,6 +497,12 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMemcpy(h->d_ford, ford.data(), sizeof(int32_t) * N, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_inv, sizeof(int32_t) * N);
     if (e == hipSuccess) e = hipMalloc(&h->d_src, sizeof(int32_t) * 8 * N);
+    std::vector<int32_t> dst(std::max<long>(1, h->llr_len), -1);
+    for (int cc = 0; cc < 8; ++cc)
+        for (int k = 0; k < N; ++k)
+            if (src[(size_t)cc * N + k] >= 0) dst[src[(size_t)cc * N + k]] = cc * N + k;
+    if (e == hipSuccess) e = hipMalloc(&h->d_dst, sizeof(int32_t) * dst.size());
+    if (e == hipSuccess) e = hipMemcpy(h->d_dst, dst.data(), sizeof(int32_t) * dst.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
     if (e == hipSuccess && TDEC_PRIO == 4) e = hipMalloc(&h->d_simd_prog, SIMD_PROG_BYTES);
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
@@ -631,6 +643,10 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_ford);
     hipFree(h->d_inv);
     hipFree(h->d_src);
+    hipFree(h->d_dst);
+    hipFree(h->d_decl);
+    hipFree(h->d_decl_n);
+    hipFree(h->d_decl_ovf);
     hipFree(h->d_tile_ctr);
     if (h->d_simd_prog) hipFree(h->d_simd_prog);
     hipFree(h->d_off);
@@ -1418,7 +1434,26 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     const int chunks = (h->N + DM_KC - 1) / DM_KC;
     const long n_items = (long)n_tiles_of(B) * chunks;   // (64-codeword tile, 16-couple chunk) pairs
     float *P = d_planes;
-    // TDEC_DM_PERSIST: one round of resident blocks (occupancy of this instance)
+    const long n_tiles = n_tiles_of(B);
+    DemapDecl dd{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};
+    if (dm_split(bps)) {   // the decline list (allocated once, flags grown with the batch)
+        if (!h->d_decl) {
+            HIPCHK(hipMalloc(&h->d_decl, sizeof(int2) * DM_DECL_CAP));
+            HIPCHK(hipMalloc(&h->d_decl_n, sizeof(unsigned)));
+        }
+        if (h->decl_tiles < n_tiles) {
+            hipFree(h->d_decl_ovf);
+            h->d_decl_ovf = nullptr;
+            h->decl_tiles = 0;
+            HIPCHK(hipMalloc(&h->d_decl_ovf, (size_t)n_tiles));
+            h->decl_tiles = n_tiles;
+        }
+        dd = DemapDecl{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};
+        HIPCHK(hipMemsetAsync(h->d_decl_n, 0, sizeof(unsigned), st));
+        HIPCHK(hipMemsetAsync(h->d_decl_ovf, 0, (size_t)n_tiles, st));
+    }
+    // TDEC_DM_PERSIST: one round of resident blocks (occupancy of this instance; the
+    // same device type throughout a process)
     static int bpc_cache[2][9];
     auto grid_of = [&](const void *kern, int f64) {
         int &bpc = bpc_cache[f64][bps];
@@ -1428,19 +1463,29 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
         const long resident = TDEC_DM_PERSIST && bpc > 0 ? (long)bpc * std::max(1, h->n_cu) : n_items;
         return dim3((unsigned)std::min(n_items, resident));
     };
+    const dim3 fgrid((unsigned)std::max<long>(1, std::min<long>(n_tiles, 1024)));
     switch (bps) {
 #define CASE(K)                                                                                              \
     case K:                                                                                                  \
-        if (cons_f64)                                                                                        \
+        if (cons_f64) {                                                                                      \
             hipLaunchKernelGGL((k_demap_planes<double, K>), grid_of((const void *)k_demap_planes<double, K>, 1),   \
                                dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
                                (const double *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off, \
-                               n_avail, P, n_items);                                                         \
-        else                                                                                                 \
+                               n_avail, P, n_items, dd);                                                     \
+            if (dm_split(K))                                                                                 \
+                hipLaunchKernelGGL((k_demap_fix<double, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,    \
+                                   (const double *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd,   \
+                                   n_tiles);                                                                 \
+        } else {                                                                                             \
             hipLaunchKernelGGL((k_demap_planes<float, K>), grid_of((const void *)k_demap_planes<float, K>, 0),     \
                                dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
                                (const float *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off,  \
-                               n_avail, P, n_items);                                                         \
+                               n_avail, P, n_items, dd);                                                     \
+            if (dm_split(K))                                                                                 \
+                hipLaunchKernelGGL((k_demap_fix<float, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,     \
+                                   (const float *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd,    \
+                                   n_tiles);                                                                 \
+        }                                                                                                    \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE

@@ -2418,18 +2418,19 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 // (:469-474; the harness pads to n_coded, test_sdr_with_coding.py:474-478).
 // src[c*N + k] = LLR index of plane component c (X.xyzw, -, -, Z.xy) or -1;
 // off[k] = first LLR index of couple k (off[N] = n_llr).
-// TDEC_DM_LEAN (round 4, square 16 / 64 / 256QAM): phase 1 runs only the fast
-// exact search (per-axis / Gray positions) and queues the symbols it declines
-// (near ties, non-finite, a non-separable table) in a compact LDS list; a second
-// loop gives those, densely packed, the rest of demap_sym's chain (the
-// sequential per-axis search, then the exact scan).  Inline in one loop, the
-// fallbacks' registers are the kernel's (256QAM: 142 VGPRs and 289 spilled
-// SGPRs against 89 for the Gray search alone).  Same planes: every path returns
-// the scan's LLRs.  Measured (profiles/r04e/ab_demap_*): the first form, a
-// bitmask and the full scan for every declined symbol, lane-sparse, was 2.3x
-// slower on 256QAM; off by default until the A/B says otherwise.
-#ifndef TDEC_DM_LEAN
-#define TDEC_DM_LEAN 0
+// TDEC_DM_SPLIT (round 4, square 16 / 64 / 256QAM): k_demap_planes runs only the
+// fast exact search (the Gray positions for 64 / 256QAM, the per-axis search for
+// 16QAM) and appends the symbols it declines (near ties, non-finite input, a
+// non-separable table: 0.02-0.08 % of them at 2 dB) to a list in HBM; k_demap_fix
+// then gives those the rest of demap_sym's chain and overwrites their plane
+// entries.  The fallbacks' registers (256QAM: 148 VGPRs and 311 SGPR spills with
+// them inline, three waves per SIMD) are then not the main kernel's.  A tile whose
+// declines overflow the list is flagged and k_demap_fix redoes all of its symbols.
+// Same planes: every path returns the scan's LLRs.  (Round 4's first form, the
+// fallback in a second loop of the same kernel, TDEC_DM_LEAN, kept the registers
+// and was 2.3x slower on 256QAM, profiles/r04e/ab_demap_*.)
+#ifndef TDEC_DM_SPLIT
+#define TDEC_DM_SPLIT 1
 #endif
 // TDEC_DM_PERSIST (build variant): k_demap_planes' grid is the device's resident
 // blocks, each looping over (tile, chunk) items with its table loaded once,
@@ -2442,30 +2443,33 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
+__host__ __device__ constexpr bool dm_split(int bps) { return TDEC_DM_SPLIT && bps >= 4 && bps % 2 == 0; }
 
-// demap_sym after the fast search declined (lean phase 2)
+// The decline list of k_demap_planes (TDEC_DM_SPLIT): entries {codeword, symbol},
+// the entry count, and per-tile overflow flags.
+constexpr unsigned DM_DECL_CAP = 1u << 21;   // entries (16 MiB): 4x the declines of 1 M 256QAM codewords at 2 dB
+struct DemapDecl {
+    int2 *list;
+    unsigned *count;
+    unsigned char *ovf;
+    unsigned cap;
+};
+
+// the fast exact search of a split table; false: declined
 template <typename T, int BPS>
-__device__ __forceinline__ void demap_fallback(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
-    if constexpr (BPS >= 8 && BPS % 2 == 0) {
-        if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return;
-    } else if constexpr (BPS >= 6 && BPS % 2 == 0) {
-        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return;
-    }
-    sym_llrs<T, BPS>(sr, si, cons, c, out);
+__device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    if constexpr (TDEC_DM_GRAY && BPS >= 6) return c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out);
+    else return c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out);
 }
 
 template <typename T, int BPS>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *__restrict__ src,
                                                        const int *__restrict__ off, long n_avail, float *planes,
-                                                       long n_items) {
+                                                       long n_items, DemapDecl dd) {
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
-    constexpr bool LEAN = TDEC_DM_LEAN && BPS >= 4 && BPS % 2 == 0;
-    constexpr int QN = LEAN ? WAVE * (DM_MAXL / BPS + 2) : 1;   // max items of a block
-    __shared__ unsigned short fl[QN];
-    __shared__ int fn;
-    if (LEAN && threadIdx.x == 0) fn = 0;
+    constexpr bool SPLIT = dm_split(BPS);
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + DM_KC - 1) / DM_KC;
     __syncthreads();
@@ -2490,13 +2494,12 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             if (cw >= B || s >= S) continue;
             const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
             double v[BPS];
-            if constexpr (LEAN) {
-                // the fast exact search: Gray positions (64 / 256QAM) or the per-axis search (16QAM)
-                bool ok;
-                if constexpr (BPS >= 6) ok = c.sep == 2 && sym_llrs_gray<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-                else ok = c.sep && sym_llrs_sep<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-                if (!ok) {
-                    fl[atomicAdd(&fn, 1)] = (unsigned short)(lane * ns + si);   // < QN
+            if constexpr (SPLIT) {
+                if (!demap_fast<T, BPS>((T)z.x, (T)z.y, cons, c, v)) {
+                    // for k_demap_fix; its plane entries are rewritten there
+                    const unsigned e = atomicAdd(dd.count, 1u);
+                    if (e < dd.cap) dd.list[e] = make_int2((int)cw, (int)s);
+                    else dd.ovf[tile] = 1;
                     continue;
                 }
             } else {
@@ -2509,24 +2512,6 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             }
         }
         __syncthreads();
-        if constexpr (LEAN) {
-            const int nq = fn;
-            for (int q = threadIdx.x; q < nq; q += BLOCK) {
-                const int it = fl[q];
-                const int ln = it / ns, sx = it - ln * ns;
-                const long cw = tile * WAVE + ln, s = s0 + sx;
-                const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
-                double v[BPS];
-                demap_fallback<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-#pragma unroll
-                for (int b = 0; b < BPS; ++b) {
-                    const long j = s * BPS + b;
-                    if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
-                }
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) fn = 0;   // ordered before the next item's queueing by the barrier below
-        }
         float *base = planes + tile * tile_floats(N);
         for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
             const int lane = t & (WAVE - 1);
@@ -2544,7 +2529,51 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
             else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
         }
-        __syncthreads();   // L (and the lean list) are rewritten by the next item
+        __syncthreads();   // L is rewritten by the next item
+    }
+}
+
+// The declined symbols of k_demap_planes (TDEC_DM_SPLIT): demap_sym's whole chain,
+// each LLR into its plane entry (dst[j] = c * N + k for the component c of couple
+// k that LLR j feeds, -1: none), then every symbol of an overflowed tile.
+template <typename T, int BPS>
+__device__ __forceinline__ void dm_fix_symbol(long cw, long s, int N, int S, const float *syms, const T *cons,
+                                              const DemapCfg &c, const int *dst, long n_avail, float *planes) {
+    const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+    double v[BPS];
+    demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+    float *base = planes + (cw / WAVE) * tile_floats(N);
+    const int lane = (int)(cw & (WAVE - 1));
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) {
+        const long j = s * BPS + b;
+        if (j >= n_avail) break;
+        const int d = dst[j];
+        if (d < 0) continue;
+        const int cc = d / N, k = d - cc * N;
+        if (cc < 4) base[((long)k * WAVE + lane) * 4 + cc] = (float)v[b];
+        else base[(long)N * WAVE * 4 + ((long)k * WAVE + lane) * 2 + (cc - 6)] = (float)v[b];
+    }
+}
+template <typename T, int BPS>
+__global__ __launch_bounds__(BLOCK) void k_demap_fix(int B, int N, int S, const float *syms, const T *cons_g,
+                                                    DemapCfg c, const int *__restrict__ dst, long n_avail,
+                                                    float *planes, DemapDecl dd, long n_tiles) {
+    __shared__ T cons[DM_TAB];
+    load_table<T, BPS>(cons, cons_g, c);
+    __syncthreads();
+    const unsigned n = min(*dd.count, dd.cap);
+    for (unsigned i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const int2 e = dd.list[i];
+        if (dd.ovf[e.x / WAVE]) continue;   // redone below
+        dm_fix_symbol<T, BPS>(e.x, e.y, N, S, syms, cons, c, dst, n_avail, planes);
+    }
+    for (long t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        if (!dd.ovf[t]) continue;
+        for (long i = threadIdx.x; i < (long)WAVE * S; i += BLOCK) {
+            const long cw = t * WAVE + i / S;
+            if (cw < B) dm_fix_symbol<T, BPS>(cw, i % S, N, S, syms, cons, c, dst, n_avail, planes);
+        }
     }
 }
 

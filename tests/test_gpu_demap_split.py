@@ -1,0 +1,94 @@
+"""The split demapper (TDEC_DM_SPLIT, csrc/tdec_kernels.hip): k_demap_planes runs
+only the fast exact search for square 16 / 64 / 256QAM and lists the symbols it
+declines; k_demap_fix gives those the full chain and rewrites their plane
+entries, and redoes every symbol of a tile whose declines overflowed the list.
+
+Checked against the host chain the reference runs (compute_llr,
+test_sdr_with_coding.py:200-225, decoder sign, truncated / zero-padded to
+n_coded, :474-478), put into the same tile planes by the depuncture kernel:
+the planes must be equal (NaN == NaN), on symbols that are declined often
+(ties, near-ties, NaN / inf, out-of-grid) and on a batch whose declines
+overflow the list (most symbols NaN)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from modulations_amd import demap as D  # noqa: E402
+from modulations_amd import dvb_rcs2_turbo as M  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _adversarial(cons, rng, shape):
+    """Noisy points mixed with exact points, bisector ties, near-ties, far / tiny /
+    huge values and NaN / inf, shuffled over the batch."""
+    n = int(np.prod(shape))
+    lv = np.unique(cons.real.astype(np.float64))
+    mids = (lv[:-1] + lv[1:]) / 2
+    k = n // 10
+    parts = [cons[rng.integers(0, len(cons), n - 7 * k)] + 0.2 * (rng.standard_normal(n - 7 * k) +
+                                                                 1j * rng.standard_normal(n - 7 * k)),
+             cons[rng.integers(0, len(cons), k)],
+             rng.choice(mids, k) + 1j * rng.choice(lv, k),
+             rng.choice(mids, k) + 1j * rng.choice(mids, k),
+             np.nextafter(rng.choice(mids, k), 9) + 1j * np.nextafter(rng.choice(mids, k), -9),
+             10 * (rng.standard_normal(k) + 1j * rng.standard_normal(k)),
+             1e-20 * (rng.standard_normal(k) + 1j * rng.standard_normal(k)),
+             rng.choice(np.array([np.nan, np.inf, -np.inf + 1j, 1 + np.nan * 1j, 3e38 + 3e38j]), k)]
+    s = np.concatenate(parts)
+    rng.shuffle(s)
+    return s.reshape(shape).astype(np.complex64)
+
+
+def _check(c, syms, mod, nv):
+    cons = D.constellation(mod)
+    bps = D.MODULATIONS[mod]["bps"]
+    B = syms.shape[0]
+    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(nv))
+    c.reserve(B)
+    planes = torch.empty(c.planes_bytes(B) // 4, dtype=torch.float32, device="cuda")
+    c.demap_planes_device(torch.from_numpy(syms).cuda(), cons, bps, nve, planes, div_f32=div32)
+    # the host chain on the distinct finite rows only (NaN symbols give NaN LLRs)
+    flat = syms.reshape(-1)
+    llr = np.full(flat.size * bps, np.nan, np.float64)
+    fin = ~np.isnan(flat)
+    llr.reshape(-1, bps)[fin] = (-O.demap(flat[fin], cons, bps, nve, div_f32=div32)).reshape(-1, bps)
+    llr = llr.reshape(B, -1)
+    ref_llr = np.zeros((B, c.n_coded), np.float32)
+    m = min(c.n_coded, llr.shape[1])
+    ref_llr[:, :m] = llr[:, :m]
+    ref = torch.empty_like(planes)
+    c.depuncture_device(torch.from_numpy(ref_llr).cuda(), ref)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(planes.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("mod,n,rate", [("16QAM", 752, "1/3"), ("64QAM", 212, "1/2"), ("256QAM", 752, "1/3"),
+                                        ("256QAM", 48, "3/4")])
+def test_split_planes_equal_host_chain(mod, n, rate):
+    rng = np.random.default_rng(sum(map(ord, mod)) + n)
+    c = M.DVBRCS2_Turbo(n, rate)
+    bps = D.MODULATIONS[mod]["bps"]
+    S = -(-c.n_coded // bps)
+    _check(c, _adversarial(D.constellation(mod), rng, (130, S)), mod, 0.04)
+
+
+def test_split_overflowing_declines_redo_their_tiles():
+    """64QAM, 8 192 codewords x 752 symbols with 90 % NaN: 5.5 M declines against
+    a list of 2 M entries, so tiles overflow and are redone whole."""
+    rng = np.random.default_rng(77)
+    mod = "64QAM"
+    c = M.DVBRCS2_Turbo(752, "1/3")
+    cons = D.constellation(mod)
+    B, S = 8192, -(-c.n_coded // 6)
+    syms = (cons[rng.integers(0, 64, (B, S))] + 0.1 * (rng.standard_normal((B, S)) +
+                                                        1j * rng.standard_normal((B, S)))).astype(np.complex64)
+    syms[rng.random((B, S)) < 0.9] = np.nan
+    _check(c, syms, mod, 0.02)

@@ -18,7 +18,7 @@ import sys
 
 def short(name):
     for k in ("k_turbo_decode_syms", "k_turbo_decode_logmap", "k_turbo_decode", "k_demap_planes", "k_workload",
-              "k_count_errors", "k_siso_spl", "k_depuncture", "k_encode", "k_siso_batch",
+              "k_count_errors", "k_siso_spl", "k_depuncture", "k_encode", "k_siso_batch", "k_demap_fix",
               "k_demap", "k_map", "k_demod", "k_fir_up", "k_fir_dec", "k_fir", "k_absmax", "k_quantize",
               "k_dequantize"):
         if k in name:

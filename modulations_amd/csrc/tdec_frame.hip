@@ -42,6 +42,16 @@ namespace tdec {
 
 constexpr int FR_WAVES = 8;
 constexpr int FR_BLOCK = FR_WAVES * WAVE;
+// TDEC_FR_WPD: waves per direction in the recursions (1, 2 or 4; see fr_recursion_x).
+// Measured (profiles/r04e/ab_frame_*, decode of N = 752 r = 1/2): 0.30 vs 0.34 ms
+// at B = 1, 0.36 vs 0.38 ms at B = 64, 1.40 vs 1.50 ms at B = 1 024: the default.
+// Four waves per direction (16 segments) halve phase A but need 5.1 rounds per SISO
+// instead of 2.8 and lose: 0.36 vs 0.29 ms at B = 1, 1.80 vs 1.39 ms at B = 1 024
+// (profiles/r04m/).
+#ifndef TDEC_FR_WPD
+#define TDEC_FR_WPD 2
+#endif
+constexpr int FR_NSEG_MAX = TDEC_FR_WPD == 4 ? 16 : 8;   // segments per direction at most
 typedef __attribute__((address_space(3))) char lds_b;   // byte-addressed LDS
 
 __device__ __forceinline__ float lds_ld(const lds_b *p) { return *(const lds_f1 *)p; }
@@ -60,7 +70,7 @@ struct FrLds {
 __host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
     FrLds L{};
     int o = 0;
-    L.ev = o;   o += 2 * 8 * 64 + 64;   // 2 directions x 8 segments; + the cross-wave rounds' control words
+    L.ev = o;   o += 2 * FR_NSEG_MAX * 64 + 64;   // 2 directions x 8 (16) segments; + the cross-wave rounds' control words
     L.sink = o; o += 2 * 512;
     L.st_a = o; o += (N + 1) * 64;
     L.st_b = o; o += (N + 1) * 64;
@@ -395,29 +405,26 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     }
 }
 
-// ---- TDEC_FR_WPD 2: 8 segments per direction on two waves each --------------------------
+// ---- TDEC_FR_WPD 2 / 4: 8 / 16 segments per direction on two / four waves each -----------
 // The same rounds as fr_recursion, with the segments of one direction spread over
 // two waves (alpha: waves 0-1, beta: waves 2-3), so each round is a workgroup step:
 // every wave (the idle ones too) passes three barriers per round -- starts read
 // before any end vector is written, rounds run, thread 0 advances both
 // directions' round state from the segments that reached their end.
-// Measured (profiles/r04e/ab_frame_*, decode of N = 752 r = 1/2): 0.30 vs 0.34 ms
-// at B = 1, 0.36 vs 0.38 ms at B = 64, 1.40 vs 1.50 ms at B = 1 024: the default.
-#ifndef TDEC_FR_WPD
-#define TDEC_FR_WPD 2
-#endif
 struct FrCtl {
     unsigned dirty[2], reached[2], state[2], broken[2], cmp[2];
 };
 enum { FR_A = 0, FR_FIX1 = 1, FR_FIXN = 2, FR_P2S = 3, FR_P2 = 4 };
 __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int lane) {
     volatile __attribute__((address_space(3))) FrCtl *ctl =
-        (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * 8 * 64);
-    const int Ls = (N + 31) / 32 * 4;       // segment length (a multiple of 4)
-    const int nseg = (N + Ls - 1) / Ls;     // 1..8
+        (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * FR_NSEG_MAX * 64);
+    constexpr int WPDX = TDEC_FR_WPD > 1 ? TDEC_FR_WPD : 2;   // waves per direction
+    static_assert(WPDX == 2 || WPDX == 4, "TDEC_FR_WPD: 1, 2 or 4");
+    const int Ls = (N + 16 * WPDX - 1) / (16 * WPDX) * 4;   // segment length (a multiple of 4)
+    const int nseg = (N + Ls - 1) / Ls;     // 1..4 * WPDX
     const unsigned all = (1u << nseg) - 1;
-    const bool rw = wave < 4;
-    const int dir = wave >> 1, wl = wave & 1, l = lane & 15, g = lane >> 4, G = 4 * wl + g;
+    const bool rw = wave < 2 * WPDX;
+    const int dir = wave / WPDX, wl = wave % WPDX, l = lane & 15, g = lane >> 4, G = 4 * wl + g;
     const int len = max(0, min(Ls, N - G * Ls)), u0 = len ? G * Ls : 0;
     if (threadIdx.x == 0)
         for (int d = 0; d < 2; ++d) {
@@ -430,7 +437,7 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
     FrLane<0> La = fr_lane<0>(l);
     FrLane<1> Lb = fr_lane<1>(l);
     const FrRec Ra{sm + Lo.st_a, sm + Lo.pmt, sm + Lo.ev, sm + Lo.sink, N};
-    const FrRec Rb{sm + Lo.st_b, sm + Lo.pmt, sm + Lo.ev + 512, sm + Lo.sink + 512, N};
+    const FrRec Rb{sm + Lo.st_b, sm + Lo.pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N};
     __syncthreads();
 #if TDEC_FR_STATS == 2
     // timers-only build: [0] ticks of round 0 (phase A), [1] of the later rounds,
@@ -660,7 +667,7 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
     // R: alpha on wave 0, beta on wave 1 (TDEC_FR_WPD 2: alpha on waves 0-1, beta on 2-3)
     if constexpr (TDEC_FR_WPD == 1) {
         if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
-        else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + 512, sm + Lo.sink + 512, N}, lane);
+        else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N}, lane);
     } else {
         fr_recursion_x(sm, Lo, N, wave, lane);
     }

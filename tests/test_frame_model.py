@@ -107,7 +107,7 @@ def lane_step(v, pm_row, ph, idx):
 def frame_recursion(pm, beta, P=4):
     """The kernel's engine: stored vectors [N][16] in step order (natural state
     order), after both passes, plus round statistics.  P segments per direction
-    (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2)."""
+    (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2; 16: four waves)."""
     N = pm.shape[0]
     lbl, idx = lane_consts(beta)
     Ls = (N + 4 * P - 1) // (4 * P) * 4
@@ -208,7 +208,7 @@ def test_lane_step_equals_serial_step(beta):
 @pytest.mark.parametrize("beta", [False, True])
 @pytest.mark.parametrize("N", [1, 2, 3, 5, 8, 13, 16, 17, 33, 48, 101, 212])
 @pytest.mark.parametrize("scale", [3.0, 1e-3])
-@pytest.mark.parametrize("P", [4, 8])
+@pytest.mark.parametrize("P", [4, 8, 16])
 def test_segment_rounds_equal_two_pass(beta, N, scale, P):
     rng = np.random.default_rng(N * 3 + int(beta))
     pm = _pm(rng, N, scale)
@@ -242,7 +242,7 @@ def test_segment_rounds_random_sweep_covers_every_path():
         if trial % 7 == 0:
             pm[rng.integers(0, N)] = np.nan
         beta = bool(trial % 2)
-        st, stats = frame_recursion(pm, beta, 8 if trial % 4 >= 2 else 4)
+        st, stats = frame_recursion(pm, beta, (4, 8, 16, 8)[trial % 4])
         np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
         seen.add((stats["spec"], stats["broken"]))
     assert {(True, False), (False, False), (False, True)} <= seen, seen

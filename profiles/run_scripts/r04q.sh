@@ -1,0 +1,8 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04q
+O=gpurun_out/r04q
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || exit 1
+TAG=r04q tools/configs.sh c2 || exit 1

@@ -938,16 +938,21 @@ placed:
 // host-pointer call, profiles/r03h_latency.jsonl, r03i_latency_lowlat4096.json):
 // B = 1 5.0 vs 11.1 ms, 256 6.7 vs 13.2 ms, 1024 9.0 vs 13.6 ms for the per-lane
 // decoder.  TDEC_LOWLAT_MAX overrides the threshold (0 disables it).
+// Round 4, the frame decoder against the throughput decoder (host-pointer calls,
+// profiles/r04u/): N = 752 r = 1/2 B = 8 192 16.3 vs 19.7 ms, 16 384 32.9 vs 26.7 ms;
+// N = 212 B = 4 096 4.3 vs 5.6 ms, 8 192 8.5 vs 6.2 ms: the threshold is 8 192 for
+// N >= 400 and 4 096 below.
 static int lowlat_max(const tdec_t *h) {
     static const int v = [] {
         const char *e = getenv("TDEC_LOWLAT_MAX");
-        return e ? std::max(0, atoi(e)) : 4096;   // crossover: profiles/r03llmax (4096: 11.6 vs 14.5 ms, 8192: 26.1 vs 20.2)
+        return e ? std::max(0, atoi(e)) : -1;
     }();
-    return h->algo == TDEC_ALGO_MAXLOG ? v : 0;
+    if (h->algo != TDEC_ALGO_MAXLOG) return 0;
+    return v >= 0 ? v : (h->N >= 400 ? 8192 : 4096);
 }
 static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // perm, inv_perm, used list
 // The frame decoder (tdec_frame.hip, one codeword per workgroup, everything in
-// LDS) takes the small batches when its LDS fits (N <= 790: every BASELINE
+// LDS) takes the small batches when its LDS fits (N <= 805: every BASELINE
 // config); the round-3 state-per-lane decoder (tdec_lowlat.hip) otherwise, or
 // with TDEC_FRAME=0 (A/B).
 static bool frame_fits(int N, bool dec) { return N <= FR_J * FR_BLOCK && fr_lds(N, dec).total <= FR_LDS_MAX; }
@@ -1436,7 +1441,8 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     float *P = d_planes;
     const long n_tiles = n_tiles_of(B);
     DemapDecl dd{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};
-    if (dm_split(bps)) {   // the decline list (allocated once, flags grown with the batch)
+    const bool split = dm_split_table(bps, h->cons.sep);
+    if (split) {   // the decline list (allocated once, flags grown with the batch)
         if (!h->d_decl) {
             HIPCHK(hipMalloc(&h->d_decl, sizeof(int2) * DM_DECL_CAP));
             HIPCHK(hipMalloc(&h->d_decl_n, sizeof(unsigned)));
@@ -1454,41 +1460,48 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     }
     // TDEC_DM_PERSIST: one round of resident blocks (occupancy of this instance; the
     // same device type throughout a process)
-    static int bpc_cache[2][9];
-    auto grid_of = [&](const void *kern, int f64) {
-        int &bpc = bpc_cache[f64][bps];
-        if (TDEC_DM_PERSIST && bpc == 0 &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, BLOCK, 0) != hipSuccess)
+    auto grid_of = [&](const void *kern, int) {
+        int bpc = 0;
+        if (TDEC_DM_PERSIST && hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, BLOCK, 0) != hipSuccess)
             bpc = -1;
         const long resident = TDEC_DM_PERSIST && bpc > 0 ? (long)bpc * std::max(1, h->n_cu) : n_items;
         return dim3((unsigned)std::min(n_items, resident));
     };
     const dim3 fgrid((unsigned)std::max<long>(1, std::min<long>(n_tiles, 1024)));
     switch (bps) {
+#define LAUNCH_PLANES(TT, K, SP, F64)                                                                     \
+    hipLaunchKernelGGL((k_demap_planes<TT, K, SP>), grid_of((const void *)k_demap_planes<TT, K, SP>, F64), dim3(BLOCK), \
+                       0, st, B, h->N, S, d_syms, (const TT *)h->cons.buf.p, c, (const int *)h->d_src,          \
+                       (const int *)h->d_off, n_avail, P, n_items, dd)
 #define CASE(K)                                                                                              \
     case K:                                                                                                  \
         if (cons_f64) {                                                                                      \
-            hipLaunchKernelGGL((k_demap_planes<double, K>), grid_of((const void *)k_demap_planes<double, K>, 1),   \
-                               dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
-                               (const double *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off, \
-                               n_avail, P, n_items, dd);                                                     \
-            if (dm_split(K))                                                                                 \
-                hipLaunchKernelGGL((k_demap_fix<double, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,    \
-                                   (const double *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd,   \
-                                   n_tiles);                                                                 \
+            if constexpr (dm_split(K)) {                                                                     \
+                if (split) {                                                                                 \
+                    LAUNCH_PLANES(double, K, dm_split(K), 1);                                                \
+                    hipLaunchKernelGGL((k_demap_fix<double, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms, \
+                                       (const double *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd, \
+                                       n_tiles);                                                             \
+                    break;                                                                                   \
+                }                                                                                            \
+            }                                                                                                \
+            LAUNCH_PLANES(double, K, false, 1);                                                              \
         } else {                                                                                             \
-            hipLaunchKernelGGL((k_demap_planes<float, K>), grid_of((const void *)k_demap_planes<float, K>, 0),     \
-                               dim3(BLOCK), 0, st, B, h->N, S, d_syms,                                       \
-                               (const float *)h->cons.buf.p, c, (const int *)h->d_src, (const int *)h->d_off,  \
-                               n_avail, P, n_items, dd);                                                     \
-            if (dm_split(K))                                                                                 \
-                hipLaunchKernelGGL((k_demap_fix<float, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,     \
-                                   (const float *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd,    \
-                                   n_tiles);                                                                 \
+            if constexpr (dm_split(K)) {                                                                     \
+                if (split) {                                                                                 \
+                    LAUNCH_PLANES(float, K, dm_split(K), 0);                                                 \
+                    hipLaunchKernelGGL((k_demap_fix<float, K>), fgrid, dim3(BLOCK), 0, st, B, h->N, S, d_syms,  \
+                                       (const float *)h->cons.buf.p, c, (const int *)h->d_dst, n_avail, P, dd,  \
+                                       n_tiles);                                                             \
+                    break;                                                                                   \
+                }                                                                                            \
+            }                                                                                                \
+            LAUNCH_PLANES(float, K, false, 0);                                                               \
         }                                                                                                    \
         break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE
+#undef LAUNCH_PLANES
     default: return fail(TDEC_EINVAL, "bps must be 1..8");
     }
     HIPCHK(hipGetLastError());

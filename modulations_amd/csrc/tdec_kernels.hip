@@ -2448,6 +2448,12 @@ __host__ __device__ constexpr bool dm_split(int bps) { return TDEC_DM_SPLIT && b
 // The decline list of k_demap_planes (TDEC_DM_SPLIT): entries {codeword, symbol},
 // the entry count, and per-tile overflow flags.
 constexpr unsigned DM_DECL_CAP = 1u << 21;   // entries (16 MiB): 4x the declines of 1 M 256QAM codewords at 2 dB
+// A table takes the split path when its fast search can accept its symbols: the
+// Gray search (64 / 256QAM) needs sep == 2, 16QAM's per-axis search sep >= 1;
+// any other table would decline every symbol.
+__host__ __device__ constexpr bool dm_split_table(int bps, int sep) {
+    return dm_split(bps) && (bps >= 6 && TDEC_DM_GRAY ? sep == 2 : sep >= 1);
+}
 struct DemapDecl {
     int2 *list;
     unsigned *count;
@@ -2462,14 +2468,14 @@ __device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const Dema
     else return c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out);
 }
 
-template <typename T, int BPS>
+template <typename T, int BPS, bool SPLIT = false>
 __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *__restrict__ src,
                                                        const int *__restrict__ off, long n_avail, float *planes,
                                                        long n_items, DemapDecl dd) {
     __shared__ T cons[DM_TAB];
     __shared__ float L[WAVE * DM_LD];
-    constexpr bool SPLIT = dm_split(BPS);
+    static_assert(!SPLIT || dm_split(BPS), "split only for square 16 / 64 / 256QAM");
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + DM_KC - 1) / DM_KC;
     __syncthreads();
@@ -2491,18 +2497,33 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             }
             const long cw = tile * WAVE + lane;
             const long s = s0 + si;
-            if (cw >= B || s >= S) continue;
-            const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+            const bool live = cw < B && s < S;
             double v[BPS];
             if constexpr (SPLIT) {
-                if (!demap_fast<T, BPS>((T)z.x, (T)z.y, cons, c, v)) {
-                    // for k_demap_fix; its plane entries are rewritten there
-                    const unsigned e = atomicAdd(dd.count, 1u);
-                    if (e < dd.cap) dd.list[e] = make_int2((int)cw, (int)s);
-                    else dd.ovf[tile] = 1;
-                    continue;
+                bool dec = false;
+                if (live) {
+                    const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
+                    dec = !demap_fast<T, BPS>((T)z.x, (T)z.y, cons, c, v);
                 }
+                // declined symbols go to the list for k_demap_fix (which rewrites their
+                // plane entries): one atomic per wave, entries by lane rank
+                const unsigned long long m = __ballot(dec);
+                if (m) {
+                    const int leader = __ffsll((long long)m) - 1, me = threadIdx.x & (WAVE - 1);
+                    unsigned base = 0;
+                    if (me == leader) base = atomicAdd(dd.count, (unsigned)__popcll(m));
+                    base = __shfl(base, leader);
+                    if (dec) {
+                        const unsigned e = base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                        if (e < dd.cap) dd.list[e] = make_int2((int)cw, (int)s);
+                        else dd.ovf[tile] = 1;
+                    }
+                }
+                if (!live || dec) continue;
             } else {
+                if (!live) continue;
+                const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
                 demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
             }
 #pragma unroll

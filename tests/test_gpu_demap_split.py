@@ -92,3 +92,36 @@ def test_split_overflowing_declines_redo_their_tiles():
                                                         1j * rng.standard_normal((B, S)))).astype(np.complex64)
     syms[rng.random((B, S)) < 0.9] = np.nan
     _check(c, syms, mod, 0.02)
+
+
+@pytest.mark.parametrize("kind", ["ring16", "natural64"])
+def test_tables_the_fast_search_cannot_take_stay_inline(kind):
+    """A 16-point two-ring table (not separable) and a 64QAM grid labelled in natural
+    binary order (separable, not Gray): the split path would decline every symbol,
+    so these run the inline chain; the planes still equal the host chain."""
+    rng = np.random.default_rng(5 if kind == "ring16" else 6)
+    if kind == "ring16":
+        cons = np.concatenate([np.exp(1j * (np.pi / 4 * np.arange(4) + np.pi / 4)),
+                               2.6 * np.exp(1j * (np.pi / 6 * np.arange(12)))]).astype(np.complex64)
+        bps = 4
+    else:
+        lv = np.arange(-7, 8, 2, dtype=np.float64) / np.sqrt(42)
+        cons = (lv[np.arange(64) >> 3] + 1j * lv[np.arange(64) & 7]).astype(np.complex64)
+        bps = 6
+    c = M.DVBRCS2_Turbo(212, "1/3")
+    B, S = 70, -(-c.n_coded // bps)
+    syms = (cons[rng.integers(0, len(cons), (B, S))] + 0.2 * (rng.standard_normal((B, S)) +
+                                                              1j * rng.standard_normal((B, S)))).astype(np.complex64)
+    syms[0, :5] = np.nan
+    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(0.05))
+    c.reserve(B)
+    planes = torch.empty(c.planes_bytes(B) // 4, dtype=torch.float32, device="cuda")
+    c.demap_planes_device(torch.from_numpy(syms).cuda(), cons, bps, nve, planes, div_f32=div32)
+    llr = np.stack([-O.demap(r, cons, bps, nve, div_f32=div32) for r in syms])
+    ref_llr = np.zeros((B, c.n_coded), np.float32)
+    m = min(c.n_coded, llr.shape[1])
+    ref_llr[:, :m] = llr[:, :m]
+    ref = torch.empty_like(planes)
+    c.depuncture_device(torch.from_numpy(ref_llr).cuda(), ref)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(planes.cpu().numpy(), ref.cpu().numpy())

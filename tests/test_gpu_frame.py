@@ -143,3 +143,18 @@ def test_frame_decode_valid_perm_round_trip():
     info = rng.integers(0, 2, (4, c.k_info))
     llr = np.stack([(1 - 2.0 * c.encode(b)) * 20.0 for b in info]).astype(np.float32)
     assert np.array_equal(c.decode_batch(llr), info)
+
+
+def test_frame_decode_at_the_routing_threshold():
+    """8 192 codewords at N = 752 (the frame decoder's batch limit for N >= 400,
+    tdec_api.hip lowlat_max): 8 192 workgroups, the largest batch it serves."""
+    rng = np.random.default_rng(8192)
+    c = M.DVBRCS2_Turbo(752, "1/2")
+    B = 8192
+    base = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in rng.integers(0, 2, (64, c.k_info))])
+    llr = (base[rng.integers(0, 64, B)] + rng.standard_normal((B, c.n_coded)) * 1.6).astype(np.float32)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    rb, rl = O.decode_batch(llr, c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
+                            c.inv_perm, TAB, want_lfinal=True, nthreads=16)
+    assert np.array_equal(bits, rb)
+    np.testing.assert_array_equal(lf, rl)

@@ -1,6 +1,8 @@
 """The low-latency (state-per-lane) max-log decoder, tdec_lowlat.hip: small
-batches (B <= 4096 by default) of DVBRCS2_Turbo.decode / decode_batch /
-decode_device run 16 lanes per codeword.  Every case is compared bit for bit
+batches of DVBRCS2_Turbo.decode / decode_batch / decode_device run 16 lanes per
+codeword where the frame decoder does not (N > 805, or TDEC_FRAME=0, which this
+module sets so that it tests this decoder; tests/test_gpu_frame.py covers the frame
+decoder).  Every case is compared bit for bit
 (hard bits and L_final, IEEE ==) with the C oracle, the restatement of
 dvb_rcs2_turbo.py:464-537 pinned to the reference's golden vectors."""
 import numpy as np
@@ -18,6 +20,18 @@ from modulations_amd import tables as T  # noqa: E402
 def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+
+
+@pytest.fixture(autouse=True)
+def _lowlat_decoder():
+    import os
+    old = os.environ.get("TDEC_FRAME")
+    os.environ["TDEC_FRAME"] = "0"   # read per call by the library
+    yield
+    if old is None:
+        os.environ.pop("TDEC_FRAME", None)
+    else:
+        os.environ["TDEC_FRAME"] = old
 
 
 def _llrs(rng, c, B, scale, noise):

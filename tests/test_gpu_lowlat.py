@@ -122,3 +122,38 @@ def test_lowlat_large_batch_matches_oracle(n, rate, interleaver):
     bits, lf = c.decode_batch(llr, return_lfinal=True)
     rb, rl = _oracle(c, llr)
     assert np.array_equal(bits, rb) and np.array_equal(lf, rl)
+
+
+def test_reserve_small_batch_on_a_block_too_long_for_the_small_batch_decoders():
+    """C ABI only (the Python codec restricts N to the standard table): N = 6 000
+    couples, beyond both the frame decoder's LDS (N <= 805) and the state-per-lane
+    decoder's 64 KiB tables (N <= 5 461).  tdec_reserve of a small batch must
+    reserve the throughput decoder's workspace, and the decode runs there, equal
+    to the oracle (one predicate for reserve and decode)."""
+    import ctypes as C
+    from modulations_amd import _native
+    L = _native.lib()
+    n, B = 6000, 3
+    perm = ((np.arange(n, dtype=np.int64) * 7 + 3) % n).astype(np.int32)   # a true permutation
+    inv = np.argsort(perm, kind="stable").astype(np.int32)
+    c = M.DVBRCS2_Turbo(48, "1/3")
+    tabs = T.packed_tables(c.next_state, c.out_W, c.out_Y, c.prev_state, c.prev_input)
+    pm = T.puncture_matrix(c.punct)
+    h = C.c_void_p()
+    assert L.tdec_create(0, n, c.punct["period"], pm.ctypes.data, 8, 0, perm.ctypes.data, inv.ctypes.data,
+                         tabs.ctypes.data, C.byref(h)) == 0, L.tdec_last_error()
+    try:
+        assert L.tdec_reserve(h, B) == 0, L.tdec_last_error()
+        rng = np.random.default_rng(6000)
+        n_coded = 6 * n   # rate 1/3: A, B, W1, Y1, W2, Y2 per couple
+        llr = (rng.standard_normal((B, n_coded)) * 2).astype(np.float32)
+        bits = np.zeros((B, 2 * n), np.int32)
+        lf = np.zeros((B, 2 * n), np.float64)
+        assert L.tdec_decode_batch(h, B, llr.ctypes.data, n_coded, bits.ctypes.data, lf.ctypes.data) == 0, \
+            L.tdec_last_error()
+    finally:
+        L.tdec_destroy(h)
+    t, _ = O.trellis()
+    rb, rl = O.decode_batch(llr, n, c.punct["period"], pm, 8, perm, inv, t, want_lfinal=True, nthreads=8)
+    assert np.array_equal(bits, rb)
+    np.testing.assert_array_equal(lf, rl)

@@ -1071,6 +1071,19 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
     return rc;
 }
 
+// Zero-copy single calls (TDEC_ZC=0 turns them off; read per call): a small
+// host-pointer call of at most ZC_MAX_ROWS rows lets the kernels read their
+// inputs from, and write their outputs to, the page-locked staging buffer itself
+// instead of a DMA each way.  Measured (profiles/r04y/, r04z/): bcjr_max_log_map
+// at N = 752 0.065 vs 0.073 ms, one decode() 0.306 vs 0.317 ms, 16 codewords
+// 0.352 vs 0.366 ms, 64 even (0.404 vs 0.41), 256 slower (0.677 vs 0.618).
+constexpr int ZC_MAX_ROWS = 64;
+static bool zero_copy(int B) {
+    const char *e = getenv("TDEC_ZC");
+    return B <= ZC_MAX_ROWS && !(e && e[0] == '0');
+}
+
+
 // Host-pointer decode in chunks, so device memory stays bounded for any B:
 // by default half the resident-wave capacity (65 536 codewords on MI355X);
 // TDEC_HOST_CHUNK overrides it (tests use a small value to exercise the chunk
@@ -1122,6 +1135,19 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
         DrainOnExit drain{h->stream, nullptr};
         char *pin = (char *)h->pin.p;
         std::memcpy(pin, llr, in_b);
+        if (zero_copy(B) && B <= lowlat_max(h) && use_frame_decoder(h)) {
+            // zero copy: the de-puncture kernel reads the LLR rows from the page-locked
+            // buffer and the frame decoder writes bits / L_final into it
+            char *dp = nullptr;
+            HIPCHK(hipHostGetDevicePointer((void **)&dp, pin, 0));
+            if ((rc = tdec_decode_batch_dev(h, B, (const float *)dp, llr_stride, (int32_t *)(dp + in_b),
+                                            lfinal ? (double *)(dp + in_b + bits_b) : nullptr, h->stream)))
+                return rc;
+            HIPCHK(hipStreamSynchronize(h->stream));
+            std::memcpy(bits, pin + in_b, bits_b);
+            if (lfinal) std::memcpy(lfinal, pin + in_b + bits_b, lf_b);
+            return 0;
+        }
         HIPCHK(hipMemcpyAsync(h->h_llr.p, pin, in_b, hipMemcpyHostToDevice, h->stream));
         if ((rc = tdec_decode_batch_dev(h, B, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
                                         lfinal ? (double *)h->h_lf.p : nullptr, h->stream)))
@@ -1278,6 +1304,24 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
             std::memcpy(pin + 3 * cf, LcY + o, nf);
             std::memcpy(pin + 4 * cf, LaA + o, nd);
             std::memcpy(pin + 4 * cf + cd, LaB + o, nd);
+            if (fr && zero_copy(n)) {
+                // zero copy: the frame SISO reads its rows from, and writes its
+                // extrinsics to, the page-locked buffer itself (each value crosses
+                // PCIe once either way: the kernel keeps its inputs in registers):
+                // no DMA in either direction
+                char *dp = nullptr;
+                HIPCHK(hipHostGetDevicePointer((void **)&dp, pin, 0));
+                FrSisoArgs fa{n, h->N, (const float *)dp, (const float *)(dp + cf), (const float *)(dp + 2 * cf),
+                              (const float *)(dp + 3 * cf), (const double *)(dp + 4 * cf),
+                              (const double *)(dp + 4 * cf + cd), sf, (double *)(dp + 4 * cf + 2 * cd),
+                              (double *)(dp + 4 * cf + 3 * cd)};
+                hipLaunchKernelGGL(k_siso_frame, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamSynchronize(s));
+                std::memcpy(LeA + o, pin + 4 * cf + 2 * cd, nd);
+                std::memcpy(LeB + o, pin + 4 * cf + 3 * cd, nd);
+                continue;
+            }
             HIPCHK(hipMemcpyAsync(base, pin, 4 * cf + 2 * cd, hipMemcpyHostToDevice, s));
         } else {
             HIPCHK(hipMemcpyAsync(dA, LcA + o, nf, hipMemcpyHostToDevice, s));

@@ -224,33 +224,44 @@ def host_api(codec, llr_rows, hb, dev):
     res["pinned"] = {"value": hb / dt, "pcie_GBps": nbytes / dt / 1e9,
                      "path": "the same call over page-locked host_buffer()s (tdec_host_alloc) for the LLRs and the bits",
                      "same_bits": bool(np.array_equal(pin_bits[:4096], codec.decode_batch(llr_h[:4096])))}
-    # single-call latency, test.py's pattern (QPSK r=1/2 N=752 frames, one decode() per frame)
-    c12 = M.DVBRCS2_Turbo(752, "1/2", 8, device=dev)
+    # single-call latency: test.py's pattern (one decode() per frame, test.py:81) and one
+    # bcjr_max_log_map call, at each BASELINE block size.  Reference: numba on one core
+    # (SURVEY §6 / BASELINE.md §2): decode 1.22 / 3.89 / 12.30 ms (r=1/3; 11.78 at 752 r=1/2);
+    # SISO 0.493 ms measured at N=752, 0.058 / 0.143 ms at N=48 / 212 derived as decode time
+    # x SISO share / 16 (76 % / 59 %).
+    ref_dec = {(48, "1/3"): 1.22, (212, "1/3"): 3.89, (752, "1/3"): 12.30, (752, "1/2"): 11.78}
+    ref_siso = {48: 0.058, 212: 0.143, 752: 0.493}
     rng = np.random.default_rng(3)
-    frames = []
-    for _ in range(21):
-        b = rng.integers(0, 2, c12.k_info)
-        frames.append(((1 - 2.0 * c12.encode(b)) * 2.0 + rng.standard_normal(c12.n_coded) * 1.5).astype(np.float32))
-    c12.decode(frames[0])                      # handle creation and workspace reserve, once
-    ts = []
-    for f in frames[1:]:
-        t0 = time.perf_counter()
-        c12.decode(f)
-        ts.append(time.perf_counter() - t0)
+    sc = {}
+    for (n, rate), ref in ref_dec.items():
+        cc = M.DVBRCS2_Turbo(n, rate, 8, device=dev)
+        frames = []
+        for _ in range(51):
+            b = rng.integers(0, 2, cc.k_info)
+            frames.append(((1 - 2.0 * cc.encode(b)) * 2.0 + rng.standard_normal(cc.n_coded) * 1.5).astype(np.float32))
+        cc.decode(frames[0])                      # handle creation and workspace reserve, once
+        ts = []
+        for f in frames[1:]:
+            t0 = time.perf_counter()
+            cc.decode(f)
+            ts.append(time.perf_counter() - t0)
+        sc[f"decode_{n}_r{rate.replace('/', '')}"] = {"ms": float(np.median(ts) * 1e3), "min_ms": float(np.min(ts) * 1e3),
+                                                    "reference_ms": ref, "x_reference": ref / float(np.median(ts) * 1e3)}
     t = M._std_tables()[:5]   # next_state, out_W, out_Y, prev_state, prev_input
-    Lc = (rng.standard_normal((4, 752)) * 3).astype(np.float32)
-    La = rng.standard_normal((2, 752)) * 5
-    M.bcjr_max_log_map(*Lc, *La, *t, 752, 0.7)
-    ts2 = []
-    for _ in range(20):
-        t0 = time.perf_counter()
-        M.bcjr_max_log_map(*Lc, *La, *t, 752, 0.7)
-        ts2.append(time.perf_counter() - t0)
-    res["single_call_ms"] = {"decode_752_r12": float(np.median(ts) * 1e3), "decode_min": float(np.min(ts) * 1e3),
-                             "bcjr_max_log_map_752": float(np.median(ts2) * 1e3),
-                             "reference_decode_ms": 12.3, "reference_siso_ms": 0.493,
-                             "path": "DVBRCS2_Turbo(752, '1/2').decode(llr) per frame as test.py:81 (median of 20); "
-                                     "bcjr_max_log_map(...) at N=752 (median of 20); reference: BASELINE.md §2"}
+    for n, ref in ref_siso.items():
+        Lc = (rng.standard_normal((4, n)) * 3).astype(np.float32)
+        La = rng.standard_normal((2, n)) * 5
+        M.bcjr_max_log_map(*Lc, *La, *t, n, 0.7)
+        ts2 = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            M.bcjr_max_log_map(*Lc, *La, *t, n, 0.7)
+            ts2.append(time.perf_counter() - t0)
+        sc[f"bcjr_max_log_map_{n}"] = {"ms": float(np.median(ts2) * 1e3), "min_ms": float(np.min(ts2) * 1e3),
+                                       "reference_ms": ref, "x_reference": ref / float(np.median(ts2) * 1e3)}
+    sc["path"] = ("DVBRCS2_Turbo(N, rate).decode(llr) per frame as test.py:81 (median of 50 noisy frames); "
+                  "bcjr_max_log_map(...) per call, f32 Lc (median of 200); reference: numba, one core, SURVEY §6")
+    res["single_call_ms"] = sc
     return res
 
 

@@ -68,6 +68,26 @@ long tdec_llr_len(const tdec_t *h);
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
                     const double *LaA, const double *LaB, double sf, double *LeA, double *LeB);
 
+/* The same SISO with float64 channel LLRs: bcjr_max_log_map as numba
+ * specialises it for float64 Lc arrays (dvb_rcs2_turbo.py:135-160, 267-268:
+ * in_A = Lc_A + La_A and the parity terms formed from the unrounded f64
+ * values, the extrinsic subtracting the f64 sum).  Float32 inputs widened to
+ * f64 give exactly tdec_siso_batch's results. */
+int tdec_siso_batch_f64(tdec_t *h, int B, const double *LcA, const double *LcB, const double *LcW,
+                        const double *LcY, const double *LaA, const double *LaB, double sf, double *LeA,
+                        double *LeB);
+
+/* The per-call form of the same SISO (one bcjr_max_log_map call is one row):
+ * tdec_siso_staging returns a page-locked buffer owned by the handle, of 8
+ * slots of *slot_bytes each (LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB: [rows][N]
+ * rows of 8-byte elements; float32 channel LLRs fill the first half of their
+ * slot).  The caller writes the six inputs there, calls tdec_siso_staged for B
+ * <= rows rows and reads LeA / LeB back from the buffer: no argument pointers,
+ * no host-side copies in the library.  The buffer stays valid until a later
+ * tdec_siso_staging call asks for more rows, or tdec_destroy. */
+int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes);
+int tdec_siso_staged(tdec_t *h, int B, int lc_f64, double sf);
+
 /* Full turbo decode of B codewords: replaces DVBRCS2_Turbo.decode
  * (dvb_rcs2_turbo.py:464-537; historic name turbo_decode).  llr rows of
  * llr_stride floats (>= tdec_llr_len), bits int32[B][2N] (A, B interleaved as

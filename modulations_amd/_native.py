@@ -28,7 +28,8 @@ EXPORTS = (
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
     "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
-    "tdec_host_alloc", "tdec_host_free", "tdec_encode_host",
+    "tdec_host_alloc", "tdec_host_free", "tdec_encode_host", "tdec_siso_batch_f64", "tdec_siso_staging",
+    "tdec_siso_staged",
 )
 
 _lib = None
@@ -49,6 +50,13 @@ def _declare(L):
     L.tdec_encoded_len.argtypes = [_vp]
     L.tdec_encoded_len.restype = C.c_long
     L.tdec_siso_batch.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_double, _vp, _vp]
+    if hasattr(L, "tdec_siso_batch_f64"):   # (A/B tools also load older builds without it)
+        L.tdec_siso_batch_f64.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_double, _vp, _vp]
+        L.tdec_siso_batch_f64.restype = C.c_int
+        L.tdec_siso_staging.argtypes = [_vp, C.c_int, C.POINTER(_vp), C.POINTER(C.c_size_t)]
+        L.tdec_siso_staging.restype = C.c_int
+        L.tdec_siso_staged.argtypes = [_vp, C.c_int, C.c_int, C.c_double]
+        L.tdec_siso_staged.restype = C.c_int
     L.tdec_decode_batch.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
     L.tdec_reserve.argtypes = [_vp, C.c_int]
     L.tdec_planes_bytes.argtypes = [_vp, C.c_int]

@@ -64,20 +64,36 @@ def build_info(out):
         return None
 
 
+def _file_sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def is_current(out, deps, extra=()):
+    """Whether `out` was built from exactly the current sources, flags and
+    compiler: its build record's src_sha256 equals the digest of what is on disk
+    now and its lib_sha256 equals the library itself.  Content, not mtimes: a
+    checkout or a copy that refreshes every mtime must not keep a stale binary,
+    and one that does not must not rebuild for nothing."""
+    info = build_info(out)
+    if not info or not os.path.exists(out):
+        return False
+    return info.get("src_sha256") == source_digest(deps, extra) and info.get("lib_sha256") == _file_sha(out)
+
+
 def _build_one(src, deps, out, force, extra):
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    if (not force and os.path.exists(out) and os.path.exists(out + ".build.json")
-            and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)):
+    if not force and is_current(out, deps, extra):
         return out
-    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", out, src]
+    tmp = out + ".tmp"
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", tmp, src]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc failed building {os.path.basename(out)}")
-    with open(out, "rb") as f:
-        lib_sha = hashlib.sha256(f.read()).hexdigest()
+    os.replace(tmp, out)   # a reader never sees a half-written library
     with open(out + ".build.json", "w") as f:
-        json.dump({"src_sha256": source_digest(deps, extra), "lib_sha256": lib_sha,
+        json.dump({"src_sha256": source_digest(deps, extra), "lib_sha256": _file_sha(out),
                    "flags": [*FLAGS, *extra]}, f, indent=1)
     return out
 
@@ -93,7 +109,9 @@ def build_modem(force=False):
 
 
 def build_variant(name, defines):
-    """Side-by-side variant for A/B timing (lib/libtdec_<name>.so)."""
+    """Side-by-side variant for A/B timing (lib/libtdec_<name>.so).  Built on
+    demand for one measurement and deleted afterwards (remove_variants): the
+    variants are not product libraries and are not pushed with the tree."""
     out = os.path.join(HERE, "lib", f"libtdec_{name}.so")
     cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"), "-o", out, SRC]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -103,8 +121,18 @@ def build_variant(name, defines):
     return out
 
 
+def remove_variants():
+    """Delete every lib/libtdec_<name>.so A/B variant."""
+    d = os.path.join(HERE, "lib")
+    for f in os.listdir(d):
+        if f.startswith("libtdec_") and f.endswith(".so"):
+            os.remove(os.path.join(d, f))
+
+
 if __name__ == "__main__":
-    if "--variant" in sys.argv:
+    if "--remove-variants" in sys.argv:
+        remove_variants()
+    elif "--variant" in sys.argv:
         i = sys.argv.index("--variant")
         print(build_variant(sys.argv[i + 1], sys.argv[i + 2:]))
     else:

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -59,21 +60,24 @@ struct DevBuf {
 };
 
 // Page-locked host staging for the small host-pointer calls (grown on demand).
+// dev: the buffer's device address (zero-copy kernels read / write it directly),
+// looked up once per allocation instead of per call.
 struct PinBuf {
-    void *p = nullptr;
+    void *p = nullptr, *dev = nullptr;
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap) return 0;
         if (p) hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         cap = 0;
         if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return fail(TDEC_ENOMEM, "hipHostMalloc failed");
+        if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) dev = nullptr;
         cap = bytes;
         return 0;
     }
     void release() {
         if (p) hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         cap = 0;
     }
 };
@@ -356,11 +360,12 @@ struct tdec_ctx {
     int cap_batch = 0;
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
     PinBuf pin;                        // page-locked staging of the small host-pointer calls
+    PinBuf pin_siso;                   // the caller-filled SISO staging (tdec_siso_staging), never regrown behind its views
+    int siso_rows = 0;                 //   rows it holds
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
-    DevBuf ll_ws, ll_st;               // low-latency decoder (state per lane): extrinsic planes, alpha / beta stores
-    int ll_cap = 0;                    // codewords the low-latency workspace holds (batches up to ll_cap - 4)
+    DevBuf ll_ws, ll_st;               // small-batch decoders: extrinsic planes (frame: Le1 only), alpha / beta stores
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // uploads of the chunked host-pointer path (created on first use)
     hipStream_t dstream = nullptr;     // its downloads (a second copy engine direction)
@@ -406,7 +411,11 @@ struct DrainOnExit {
         if (a) hipStreamSynchronize(a);
         if (b && b != a) hipStreamSynchronize(b);
     }
+    void disarm() { a = b = nullptr; }   // the call synchronised its streams itself
 };
+// A host-pointer call that synchronised its stream leaves nothing queued on the
+// handle's buffers: no event to record (mark_used) and none to wait on later.
+void mark_idle(tdec_ctx *h) { h->pending = false; }
 }  // namespace
 
 extern "C" {
@@ -659,6 +668,7 @@ void tdec_destroy(tdec_t *h) {
     h->h_lf.release();
     h->h_misc.release();
     h->pin.release();
+    h->pin_siso.release();
     h->cons.buf.release();
     h->spl_ck.release();
     h->planes_w.release();
@@ -942,14 +952,6 @@ placed:
 // profiles/r04u/): N = 752 r = 1/2 B = 8 192 16.3 vs 19.7 ms, 16 384 32.9 vs 26.7 ms;
 // N = 212 B = 4 096 4.3 vs 5.6 ms, 8 192 8.5 vs 6.2 ms: the threshold is 8 192 for
 // N >= 400 and 4 096 below.
-static int lowlat_max(const tdec_t *h) {
-    static const int v = [] {
-        const char *e = getenv("TDEC_LOWLAT_MAX");
-        return e ? std::max(0, atoi(e)) : -1;
-    }();
-    if (h->algo != TDEC_ALGO_MAXLOG) return 0;
-    return v >= 0 ? v : (h->N >= 400 ? 8192 : 4096);
-}
 static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // perm, inv_perm, used list
 // The frame decoder (tdec_frame.hip, one codeword per workgroup, everything in
 // LDS) takes the small batches when its LDS fits (N <= 805: every BASELINE
@@ -960,32 +962,71 @@ static bool use_frame_decoder(const tdec_t *h) {
     const char *e = getenv("TDEC_FRAME");   // read per call: tests switch decoders in-process
     return !(e && e[0] == '0') && frame_fits(h->N, true);
 }
+static int lowlat_max(const tdec_t *h) {
+    static const int v = [] {
+        const char *e = getenv("TDEC_LOWLAT_MAX");
+        return e ? std::max(0, atoi(e)) : -1;
+    }();
+    if (h->algo != TDEC_ALGO_MAXLOG) return 0;
+    if (v >= 0) return v;
+    // 8 192 was measured for the frame decoder only; the state-per-lane decoder's
+    // own crossover is 4 096 (26.1 vs 20.2 ms at 8 192, profiles/r03llmax/)
+    return h->N >= 400 && use_frame_decoder(h) ? 8192 : 4096;
+}
 // One predicate for "the small-batch decoders can run on this handle" (reserve and decode).
 static bool lowlat_usable(const tdec_t *h) {
     return lowlat_max(h) > 0 && (use_frame_decoder(h) || ll_lds_bytes(h->N) <= 64 * 1024);
 }
-static bool use_lowlat(const tdec_t *h, int B) {
-    return B <= lowlat_max(h) && B + 4 <= h->ll_cap && lowlat_usable(h);
+// Codewords the small-batch workspace holds for the decoder that would run (batches
+// up to that minus 4): the frame decoder keeps only Le1 (N double2 per row) outside
+// LDS, the state-per-lane decoder three extrinsic planes and the alpha / beta stores.
+static int ll_cap_of(const tdec_t *h) {
+    if (use_frame_decoder(h)) return (int)std::min<size_t>(h->ll_ws.cap / ((size_t)h->N * sizeof(double2)), 1 << 30);
+    return (int)std::min(h->ll_ws.cap / (ll_ws_elems(h->N) * sizeof(double2)), h->ll_st.cap / (ll_st_elems(h->N) * sizeof(float)));
 }
-// kernels with more than 64 KiB of dynamic LDS must say so once
-static int frame_lds_attr() {
-    static const hipError_t e = [] {
-        hipError_t r = hipFuncSetAttribute((const void *)k_turbo_decode_frame, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           FR_LDS_MAX);
-        if (r == hipSuccess)
-            r = hipFuncSetAttribute((const void *)k_siso_frame, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
-        return r;
-    }();
-    if (e != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(e));
+static bool use_lowlat(const tdec_t *h, int B) {
+    return B <= lowlat_max(h) && B + 4 <= ll_cap_of(h) && lowlat_usable(h);
+}
+// kernels with more than 64 KiB of dynamic LDS must say so, once per device (the
+// attribute belongs to the kernel on the device current when it is set)
+static int frame_lds_attr(int device) {
+    static std::mutex mu;
+    static unsigned char done[256];
+    if (device < 0 || device >= 256) return fail(TDEC_EINVAL, "device ordinal out of range");
+    std::lock_guard<std::mutex> lk(mu);
+    if (done[device]) return 0;
+    const void *fns[] = {(const void *)k_turbo_decode_frame, (const void *)k_siso_frame<float>,
+                         (const void *)k_siso_frame<double>};
+    for (const void *f : fns) {
+        const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
+        if (r != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(r));
+    }
+    done[device] = 1;
     return 0;
 }
 
 static int ensure_lowlat(tdec_t *h, int B) {
-    if (B > lowlat_max(h) || B + 4 <= h->ll_cap || !lowlat_usable(h)) return 0;
-    const int cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
-    if (int rc = h->ll_ws.ensure((size_t)cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
-    if (int rc = h->ll_st.ensure((size_t)cap * ll_st_elems(h->N) * sizeof(float))) return rc;
-    h->ll_cap = cap;
+    if (B > lowlat_max(h) || B + 4 <= ll_cap_of(h) || !lowlat_usable(h)) return 0;
+    const size_t cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
+    if (use_frame_decoder(h)) return h->ll_ws.ensure(cap * h->N * sizeof(double2));
+    if (int rc = h->ll_ws.ensure(cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
+    return h->ll_st.ensure(cap * ll_st_elems(h->N) * sizeof(float));
+}
+
+// k_demap_planes' decline list (entries + count, allocated once) and its per-tile
+// overflow flags (grown with the batch).  The caller has quiesced the handle.
+static int ensure_decl(tdec_t *h, long n_tiles) {
+    if (!h->d_decl) {
+        HIPCHK(hipMalloc(&h->d_decl, sizeof(int2) * DM_DECL_CAP));
+        HIPCHK(hipMalloc(&h->d_decl_n, sizeof(unsigned)));
+    }
+    if (h->decl_tiles < n_tiles) {
+        hipFree(h->d_decl_ovf);
+        h->d_decl_ovf = nullptr;
+        h->decl_tiles = 0;
+        HIPCHK(hipMalloc(&h->d_decl_ovf, (size_t)n_tiles));
+        h->decl_tiles = n_tiles;
+    }
     return 0;
 }
 
@@ -994,16 +1035,21 @@ int tdec_reserve(tdec_t *h, int max_batch) {
     if (max_batch == 0) return 0;
     Guard g(h->device);
     if (max_batch <= lowlat_max(h) && lowlat_usable(h)) {   // small batches: the frame / state-per-lane decoders' workspace only
-        if (max_batch + 4 > h->ll_cap || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);
+        if (max_batch + 4 > ll_cap_of(h) || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);
+        if (n_tiles_of(max_batch) > h->decl_tiles) quiesce(h);
         int rc = ensure_lowlat(h, max_batch);
         if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
+        if (!rc) rc = ensure_decl(h, n_tiles_of(max_batch));   // the demapper's, for tdec_demap_planes_dev
         if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
         return rc;
     }
     const int want_waves = std::min(n_tiles_of(max_batch), h->max_waves);
-    if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap) quiesce(h);   // regrowth frees
+    if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap ||
+        n_tiles_of(max_batch) > h->decl_tiles)
+        quiesce(h);   // regrowth frees
     int rc = ensure_ws(h, want_waves);
     if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
+    if (!rc) rc = ensure_decl(h, n_tiles_of(max_batch));
     if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
     return rc;
 }
@@ -1031,7 +1077,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     if (use_lowlat(h, B)) {
         if (int rc = order_on(h, st)) return rc;
         if (use_frame_decoder(h)) {
-            if (int rc = frame_lds_attr()) return rc;
+            if (int rc = frame_lds_attr(h->device)) return rc;
             FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used};
             hipLaunchKernelGGL(k_turbo_decode_frame, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true).total, st, a,
                                (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ford);
@@ -1125,38 +1171,45 @@ int tdec_decode_batch(tdec_t *h, int B, const float *llr, long llr_stride, int32
     // the pipeline's event setup were most of a per-frame call.
     const size_t in_b = (size_t)B * llr_stride * sizeof(float), bits_b = (size_t)B * 2 * h->N * sizeof(int32_t),
                  lf_b = lfinal ? (size_t)B * 2 * h->N * sizeof(double) : 0;
-    if (n_chunks == 1 && in_b + bits_b + lf_b <= SMALL_CALL_BYTES) {
+    // page-locked layout: LLR rows, bits, L_final, each at a 256-B boundary (the
+    // zero-copy kernels store int2 / double2 there whatever the row stride)
+    auto up256 = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_bits = up256(in_b), o_lf = up256(o_bits + bits_b), pin_b = o_lf + lf_b;
+    if (n_chunks == 1 && pin_b <= SMALL_CALL_BYTES) {
         int rc = tdec_reserve(h, B);
         if (!rc) rc = h->h_llr.ensure(in_b);
         if (!rc) rc = h->h_bits.ensure(bits_b);
         if (!rc && lfinal) rc = h->h_lf.ensure(lf_b);
-        if (!rc) rc = h->pin.ensure(in_b + bits_b + lf_b);
+        if (!rc) rc = h->pin.ensure(pin_b);
         if (rc) return rc;
         DrainOnExit drain{h->stream, nullptr};
         char *pin = (char *)h->pin.p;
         std::memcpy(pin, llr, in_b);
-        if (zero_copy(B) && B <= lowlat_max(h) && use_frame_decoder(h)) {
+        if (zero_copy(B) && use_lowlat(h, B) && use_frame_decoder(h) && h->pin.dev) {
             // zero copy: the de-puncture kernel reads the LLR rows from the page-locked
             // buffer and the frame decoder writes bits / L_final into it
-            char *dp = nullptr;
-            HIPCHK(hipHostGetDevicePointer((void **)&dp, pin, 0));
-            if ((rc = tdec_decode_batch_dev(h, B, (const float *)dp, llr_stride, (int32_t *)(dp + in_b),
-                                            lfinal ? (double *)(dp + in_b + bits_b) : nullptr, h->stream)))
+            char *dp = (char *)h->pin.dev;
+            if ((rc = tdec_decode_batch_dev(h, B, (const float *)dp, llr_stride, (int32_t *)(dp + o_bits),
+                                            lfinal ? (double *)(dp + o_lf) : nullptr, h->stream)))
                 return rc;
             HIPCHK(hipStreamSynchronize(h->stream));
-            std::memcpy(bits, pin + in_b, bits_b);
-            if (lfinal) std::memcpy(lfinal, pin + in_b + bits_b, lf_b);
+            drain.disarm();
+            mark_idle(h);
+            std::memcpy(bits, pin + o_bits, bits_b);
+            if (lfinal) std::memcpy(lfinal, pin + o_lf, lf_b);
             return 0;
         }
         HIPCHK(hipMemcpyAsync(h->h_llr.p, pin, in_b, hipMemcpyHostToDevice, h->stream));
         if ((rc = tdec_decode_batch_dev(h, B, (const float *)h->h_llr.p, llr_stride, (int32_t *)h->h_bits.p,
                                         lfinal ? (double *)h->h_lf.p : nullptr, h->stream)))
             return rc;
-        HIPCHK(hipMemcpyAsync(pin + in_b, h->h_bits.p, bits_b, hipMemcpyDeviceToHost, h->stream));
-        if (lfinal) HIPCHK(hipMemcpyAsync(pin + in_b + bits_b, h->h_lf.p, lf_b, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(pin + o_bits, h->h_bits.p, bits_b, hipMemcpyDeviceToHost, h->stream));
+        if (lfinal) HIPCHK(hipMemcpyAsync(pin + o_lf, h->h_lf.p, lf_b, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
-        std::memcpy(bits, pin + in_b, bits_b);
-        if (lfinal) std::memcpy(lfinal, pin + in_b + bits_b, lf_b);
+        drain.disarm();
+        mark_idle(h);
+        std::memcpy(bits, pin + o_bits, bits_b);
+        if (lfinal) std::memcpy(lfinal, pin + o_lf, lf_b);
         return 0;
     }
     const int nbuf = n_chunks > 1 ? 2 : 1;
@@ -1259,8 +1312,61 @@ int tdec_demap_stats(unsigned long long *out) {
 }
 #endif
 
-int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
-                    const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {
+}  // extern "C"
+
+// One SISO launch over n rows already in device-visible memory (device buffers, or
+// the page-locked staging's device view for the zero-copy frame kernel).
+template <typename T>
+static int siso_launch(tdec_t *h, int n, const T *A, const T *B, const T *W, const T *Y, const double *la,
+                       const double *lb, double sf, double *ea, double *eb, bool fr, bool spl, hipStream_t s) {
+    constexpr bool F64 = sizeof(T) == 8;
+    if (fr) {
+        FrSisoArgs fa{n, h->N, A, B, W, Y, la, lb, sf, ea, eb};
+        hipLaunchKernelGGL(k_siso_frame<T>, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    const int nwv = n_tiles_of(n);
+    if (spl) {   // A/B prototype: one state per lane, 4 codewords per wave (tdec_spl.hip)
+        const long sw = (n + 3) / 4;                     // waves
+        const long stride = ((h->N + SPL_W - 1) / SPL_W + RING) * 64L;
+        if (int rc = h->spl_ck.ensure(sizeof(float) * stride * ((sw + 3) / 4 * 4))) return rc;
+        SplArgs sa{n, h->N, (const float *)A, (const float *)B, (const float *)W, (const float *)Y, la, lb, sf, ea, eb,
+                   (float *)h->spl_ck.p, stride};
+        hipLaunchKernelGGL(k_siso_spl, dim3((unsigned)((sw + 3) / 4)), dim3(256), 0, s, sa);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    SisoArgs a{};
+    a.B = n, a.N = h->N, a.n_waves = nwv, a.LaA = la, a.LaB = lb, a.sf = sf, a.LeA = ea, a.LeB = eb;
+    a.ck = h->ck_p, a.ck_stride = ck_stride_of(h);
+    if constexpr (F64) a.Lc64A = A, a.Lc64B = B, a.Lc64W = W, a.Lc64Y = Y;
+    else a.LcA = A, a.LcB = B, a.LcW = W, a.LcY = Y;
+    const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
+    if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true, F64>), grid, dim3(BLOCK), 0, s, a);
+    else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false, F64>), grid, dim3(BLOCK), 0, s, a);
+    else if (rag) hipLaunchKernelGGL((k_siso_batch<true, F64>), grid, dim3(BLOCK), 0, s, a);
+    else hipLaunchKernelGGL((k_siso_batch<false, F64>), grid, dim3(BLOCK), 0, s, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// Which SISO kernel serves a handle: max-log rows go to the frame SISO (one row per
+// workgroup, tdec_frame.hip; no workspace) unless TDEC_SISO_FRAME=0 (A/B) or its LDS
+// does not fit; TDEC_SISO_SPL=1 selects the state-per-lane prototype (float32 only).
+static void siso_route(const tdec_t *h, bool f64, bool &fr, bool &spl) {
+    const char *se = getenv("TDEC_SISO_SPL");
+    spl = !f64 && se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
+    const char *sfe = getenv("TDEC_SISO_FRAME");
+    fr = !spl && h->algo == TDEC_ALGO_MAXLOG && !(sfe && sfe[0] == '0') && frame_fits(h->N, false);
+}
+
+// tdec_siso_batch / tdec_siso_batch_f64: T = the channel LLRs' dtype.
+template <typename T>
+static int siso_batch_impl(tdec_t *h, int B, const T *LcA, const T *LcB, const T *LcW, const T *LcY, const double *LaA,
+                           const double *LaB, double sf, double *LeA, double *LeB) {
+    constexpr bool F64 = sizeof(T) == 8;
     if (!h || B < 0) return fail(TDEC_EINVAL, "bad siso arguments");
     if (B == 0) return 0;
     if (!LcA || !LcB || !LcW || !LcY || !LaA || !LaB || !LeA || !LeB) return fail(TDEC_EINVAL, "bad siso arguments");
@@ -1271,31 +1377,26 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
     long chunk = 4L * h->max_waves * WAVE;
     if (const char *pc = getenv("TDEC_HOST_CHUNK")) chunk = std::max(1L, atol(pc));
     const int C = (int)std::min<long>(B, chunk), waves = n_tiles_of(C);
-    const size_t N = h->N, cf = (size_t)C * N * sizeof(float), cd = (size_t)C * N * sizeof(double);
-    const char *se = getenv("TDEC_SISO_SPL");
-    const bool spl = se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
-    // max-log rows go to the frame SISO (one row per workgroup, tdec_frame.hip; no
-    // workspace) unless TDEC_SISO_FRAME=0 (A/B) or its LDS does not fit
-    const char *sfe = getenv("TDEC_SISO_FRAME");
-    const bool fr = !spl && h->algo == TDEC_ALGO_MAXLOG && !(sfe && sfe[0] == '0') && frame_fits(h->N, false);
-    int rc = fr ? frame_lds_attr() : ensure_ws(h, waves);
+    const size_t N = h->N, cf = (size_t)C * N * sizeof(T), cd = (size_t)C * N * sizeof(double);
+    bool fr, spl;
+    siso_route(h, F64, fr, spl);
+    int rc = fr ? frame_lds_attr(h->device) : ensure_ws(h, waves);
     if (!rc) rc = h->h_misc.ensure(4 * cf + 4 * cd);
     if (rc) return rc;
     char *base = (char *)h->h_misc.p;
-    float *dA = (float *)base, *dB = (float *)(base + cf), *dW = (float *)(base + 2 * cf), *dY = (float *)(base + 3 * cf);
+    T *dA = (T *)base, *dB = (T *)(base + cf), *dW = (T *)(base + 2 * cf), *dY = (T *)(base + 3 * cf);
     double *daA = (double *)(base + 4 * cf), *daB = (double *)(base + 4 * cf + cd);
     double *deA = (double *)(base + 4 * cf + 2 * cd), *deB = (double *)(base + 4 * cf + 3 * cd);
     hipStream_t s = h->stream;
-    const bool rag = h->N % WIN != 0;   // the row SISO runs siso<> at WIN
-    // small calls (a bcjr_max_log_map call is one row): the six inputs packed into one
-    // page-locked buffer laid out as the device staging, one DMA each way
+    // small calls: the six inputs packed into one page-locked buffer laid out as the
+    // device staging, one DMA each way
     const bool small = B <= C && 4 * cf + 4 * cd <= SMALL_CALL_BYTES;
     if (small) {
         if (int rc = h->pin.ensure(4 * cf + 4 * cd)) return rc;
     }
     for (long r0 = 0; r0 < B; r0 += C) {
-        const int n = (int)std::min<long>(C, B - r0), nwv = n_tiles_of(n);
-        const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(float), nd = (size_t)n * N * sizeof(double);
+        const int n = (int)std::min<long>(C, B - r0);
+        const size_t o = (size_t)r0 * N, nf = (size_t)n * N * sizeof(T), nd = (size_t)n * N * sizeof(double);
         if (small) {
             char *pin = (char *)h->pin.p;
             std::memcpy(pin, LcA + o, nf);
@@ -1304,19 +1405,17 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
             std::memcpy(pin + 3 * cf, LcY + o, nf);
             std::memcpy(pin + 4 * cf, LaA + o, nd);
             std::memcpy(pin + 4 * cf + cd, LaB + o, nd);
-            if (fr && zero_copy(n)) {
+            if (fr && zero_copy(n) && h->pin.dev) {
                 // zero copy: the frame SISO reads its rows from, and writes its
                 // extrinsics to, the page-locked buffer itself (each value crosses
                 // PCIe once either way: the kernel keeps its inputs in registers):
                 // no DMA in either direction
-                char *dp = nullptr;
-                HIPCHK(hipHostGetDevicePointer((void **)&dp, pin, 0));
-                FrSisoArgs fa{n, h->N, (const float *)dp, (const float *)(dp + cf), (const float *)(dp + 2 * cf),
-                              (const float *)(dp + 3 * cf), (const double *)(dp + 4 * cf),
-                              (const double *)(dp + 4 * cf + cd), sf, (double *)(dp + 4 * cf + 2 * cd),
-                              (double *)(dp + 4 * cf + 3 * cd)};
-                hipLaunchKernelGGL(k_siso_frame, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
-                HIPCHK(hipGetLastError());
+                char *dp = (char *)h->pin.dev;
+                if (int rc = siso_launch<T>(h, n, (const T *)dp, (const T *)(dp + cf), (const T *)(dp + 2 * cf),
+                                            (const T *)(dp + 3 * cf), (const double *)(dp + 4 * cf),
+                                            (const double *)(dp + 4 * cf + cd), sf, (double *)(dp + 4 * cf + 2 * cd),
+                                            (double *)(dp + 4 * cf + 3 * cd), true, false, s))
+                    return rc;
                 HIPCHK(hipStreamSynchronize(s));
                 std::memcpy(LeA + o, pin + 4 * cf + 2 * cd, nd);
                 std::memcpy(LeB + o, pin + 4 * cf + 3 * cd, nd);
@@ -1331,22 +1430,7 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
             HIPCHK(hipMemcpyAsync(daA, LaA + o, nd, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemcpyAsync(daB, LaB + o, nd, hipMemcpyHostToDevice, s));
         }
-        SisoArgs a{n, h->N, nwv, dA, dB, dW, dY, daA, daB, sf, deA, deB, h->ck_p, ck_stride_of(h)};
-        const dim3 grid((nwv + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-        if (fr) {
-            FrSisoArgs fa{n, h->N, dA, dB, dW, dY, daA, daB, sf, deA, deB};
-            hipLaunchKernelGGL(k_siso_frame, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
-        } else if (spl) {   // A/B prototype: one state per lane, 4 codewords per wave (tdec_spl.hip)
-            const long sw = (n + 3) / 4;                     // waves
-            const long stride = ((h->N + SPL_W - 1) / SPL_W + RING) * 64L;
-            if (int rc = h->spl_ck.ensure(sizeof(float) * stride * ((sw + 3) / 4 * 4))) return rc;
-            SplArgs sa{n, h->N, dA, dB, dW, dY, daA, daB, sf, deA, deB, (float *)h->spl_ck.p, stride};
-            hipLaunchKernelGGL(k_siso_spl, dim3((unsigned)((sw + 3) / 4)), dim3(256), 0, s, sa);
-        } else if (h->algo && rag) hipLaunchKernelGGL((k_siso_batch_logmap<true>), grid, dim3(BLOCK), 0, s, a);
-        else if (h->algo) hipLaunchKernelGGL((k_siso_batch_logmap<false>), grid, dim3(BLOCK), 0, s, a);
-        else if (rag) hipLaunchKernelGGL((k_siso_batch<true>), grid, dim3(BLOCK), 0, s, a);
-        else hipLaunchKernelGGL((k_siso_batch<false>), grid, dim3(BLOCK), 0, s, a);
-        HIPCHK(hipGetLastError());
+        if (int rc = siso_launch<T>(h, n, dA, dB, dW, dY, daA, daB, sf, deA, deB, fr, spl, s)) return rc;
         if (small) {
             char *pin = (char *)h->pin.p + 4 * cf + 2 * cd;
             HIPCHK(hipMemcpyAsync(pin, deA, 2 * cd, hipMemcpyDeviceToHost, s));   // deB follows deA
@@ -1359,7 +1443,78 @@ int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const 
             HIPCHK(hipStreamSynchronize(s));
         }
     }
-    return mark_used(h, s);
+    drain.disarm();   // every chunk ended in a synchronisation of the handle's stream
+    mark_idle(h);
+    return 0;
+}
+
+// The caller-filled staging of small SISO calls: 8 slots [rows][N] of 8-byte
+// elements (LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB), each at a 256-B boundary; a
+// float32 channel-LLR row uses the first half of its slot.
+static size_t siso_slot(const tdec_t *h, int rows) { return ((size_t)rows * h->N * 8 + 255) / 256 * 256; }
+
+template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
+    constexpr bool F64 = sizeof(T) == 8;
+    if (!h || B < 1 || B > h->siso_rows || !h->pin_siso.p) return fail(TDEC_EINVAL, "bad staged siso call (tdec_siso_staging first)");
+    Guard g(h->device);
+    quiesce(h);
+    DrainOnExit drain{h->stream, nullptr};
+    bool fr, spl;
+    siso_route(h, F64, fr, spl);
+    int rc = fr ? frame_lds_attr(h->device) : ensure_ws(h, n_tiles_of(B));
+    const size_t sl = siso_slot(h, h->siso_rows);
+    if (!rc && !(fr && zero_copy(B) && h->pin_siso.dev)) rc = h->h_misc.ensure(8 * sl);
+    if (rc) return rc;
+    hipStream_t s = h->stream;
+    char *dp;
+    if (fr && zero_copy(B) && h->pin_siso.dev) {
+        dp = (char *)h->pin_siso.dev;   // the kernel reads and writes the page-locked slots
+    } else {
+        dp = (char *)h->h_misc.p;
+        HIPCHK(hipMemcpyAsync(dp, h->pin_siso.p, 6 * sl, hipMemcpyHostToDevice, s));
+    }
+    if ((rc = siso_launch<T>(h, B, (const T *)dp, (const T *)(dp + sl), (const T *)(dp + 2 * sl), (const T *)(dp + 3 * sl),
+                             (const double *)(dp + 4 * sl), (const double *)(dp + 5 * sl), sf, (double *)(dp + 6 * sl),
+                             (double *)(dp + 7 * sl), fr, spl, s)))
+        return rc;
+    if (dp == (char *)h->h_misc.p)
+        HIPCHK(hipMemcpyAsync((char *)h->pin_siso.p + 6 * sl, dp + 6 * sl, 2 * sl, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    drain.disarm();
+    mark_idle(h);
+    return 0;
+}
+
+extern "C" {
+
+int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes) {
+    if (!h || rows < 1 || !buf || !slot_bytes) return fail(TDEC_EINVAL, "bad siso staging arguments");
+    Guard g(h->device);
+    if (rows > h->siso_rows) {
+        quiesce(h);
+        h->pin_siso.release();   // the caller's views of the old buffer die with this call
+        h->siso_rows = 0;
+        if (int rc = h->pin_siso.ensure(8 * siso_slot(h, rows))) return rc;
+        h->siso_rows = rows;
+    }
+    *buf = h->pin_siso.p;
+    *slot_bytes = siso_slot(h, h->siso_rows);
+    return 0;
+}
+
+int tdec_siso_staged(tdec_t *h, int B, int lc_f64, double sf) {
+    return lc_f64 ? siso_staged_impl<double>(h, B, sf) : siso_staged_impl<float>(h, B, sf);
+}
+
+int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
+                    const double *LaA, const double *LaB, double sf, double *LeA, double *LeB) {
+    return siso_batch_impl<float>(h, B, LcA, LcB, LcW, LcY, LaA, LaB, sf, LeA, LeB);
+}
+
+int tdec_siso_batch_f64(tdec_t *h, int B, const double *LcA, const double *LcB, const double *LcW,
+                        const double *LcY, const double *LaA, const double *LaB, double sf, double *LeA,
+                        double *LeB) {
+    return siso_batch_impl<double>(h, B, LcA, LcB, LcW, LcY, LaA, LaB, sf, LeA, LeB);
 }
 
 int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, const void *cons, int cons_f64, int M,
@@ -1486,17 +1641,14 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     const long n_tiles = n_tiles_of(B);
     DemapDecl dd{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};
     const bool split = dm_split_table(bps, h->cons.sep);
-    if (split) {   // the decline list (allocated once, flags grown with the batch)
-        if (!h->d_decl) {
-            HIPCHK(hipMalloc(&h->d_decl, sizeof(int2) * DM_DECL_CAP));
-            HIPCHK(hipMalloc(&h->d_decl_n, sizeof(unsigned)));
-        }
+    if (split) {   // the decline list: sized by tdec_reserve / tdec_reserve_fused
         if (h->decl_tiles < n_tiles) {
-            hipFree(h->d_decl_ovf);
-            h->d_decl_ovf = nullptr;
-            h->decl_tiles = 0;
-            HIPCHK(hipMalloc(&h->d_decl_ovf, (size_t)n_tiles));
-            h->decl_tiles = n_tiles;
+            // an unreserved batch: allocate here, outside any stream capture (hipFree
+            // synchronises the device, and a captured graph must not hold a buffer
+            // freed by a later regrowth)
+            if (capturing(st)) return fail(TDEC_ECAPACITY, "demap batch larger than tdec_reserve() (stream capture)");
+            quiesce(h);
+            if (int rc = ensure_decl(h, n_tiles)) return rc;
         }
         dd = DemapDecl{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};
         HIPCHK(hipMemsetAsync(h->d_decl_n, 0, sizeof(unsigned), st));

@@ -621,7 +621,7 @@ struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[
     typedef float4 Raw;
     const lds_b *le2;
     const lds_int *inv;
-    __device__ __forceinline__ void get(const Raw &x, int k, double &iA, double &iB, float &w, float &y, float &la,
+    __device__ __forceinline__ void get(const Raw &x, int k, double &iA, double &iB, double &w, double &y, float &la,
                                         float &lb) const {
         const d2v p = *(const lds_d2 *)(le2 + 16 * inv[k]);
         iA = (double)x.x + p.x;
@@ -636,7 +636,7 @@ struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 
     typedef float2 Raw;
     const lds_b *p1;
     const lds_int *perm;
-    __device__ __forceinline__ void get(const Raw &z, int k, double &iA, double &iB, float &w, float &y, float &la,
+    __device__ __forceinline__ void get(const Raw &z, int k, double &iA, double &iB, double &w, double &y, float &la,
                                         float &lb) const {
         const d2v p = *(const lds_d2 *)(p1 + 16 * perm[k]);
         iA = p.x;
@@ -646,16 +646,18 @@ struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 
         la = lb = 0.0f;
     }
 };
-struct FrRowRaw {
-    float a, b, w, y;
+// bcjr_max_log_map's arguments (:116), one row; T = the channel LLRs' dtype
+// (float32, or float64: numba's f64 specialisation, sums from unrounded values)
+template <typename T> struct FrRowRaw {
+    T a, b, w, y;
     double la, lb;
 };
-struct FrInRow {   // bcjr_max_log_map's arguments (:116), one row
-    typedef FrRowRaw Raw;
-    const float *A, *B, *W, *Y;
+template <typename T> struct FrInRow {
+    typedef FrRowRaw<T> Raw;
+    const T *A, *B, *W, *Y;
     const double *LaA, *LaB;
     __device__ __forceinline__ Raw fetch(int k) const { return Raw{A[k], B[k], W[k], Y[k], LaA[k], LaB[k]}; }
-    __device__ __forceinline__ void get(const Raw &r, int, double &iA, double &iB, float &w, float &y, float &la,
+    __device__ __forceinline__ void get(const Raw &r, int, double &iA, double &iB, double &w, double &y, float &la,
                                         float &lb) const {
         iA = (double)r.a + r.la;
         iB = (double)r.b + r.lb;
@@ -705,8 +707,8 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
     for (int j = 0; j < FR_J; ++j) {
         const int k = pos[j];
         if (k < 0) continue;
-        double iA, iB;
-        float w, y, la, lb;
+        double iA, iB, w, y;
+        float la, lb;
         in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8], pm[2][4];
         gamma_from_sums(iA, iB, w, y, g);
@@ -736,8 +738,8 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
     for (int j = 0; j < FR_J; ++j) {
         const int k = pos[j];
         if (k < 0 || tid + j * FR_BLOCK >= M) continue;
-        double iA, iB;
-        float w, y, la, lb;
+        double iA, iB, w, y;
+        float la, lb;
         in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8];
         gamma_from_sums(iA, iB, w, y, g);
@@ -832,18 +834,19 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
 // bcjr_max_log_map (:116-281) on [B][N] rows, one row per workgroup.
 struct FrSisoArgs {
     int B, N;
-    const float *LcA, *LcB, *LcW, *LcY;
+    const void *LcA, *LcB, *LcW, *LcY;   // float32, or float64 for k_siso_frame<double>
     const double *LaA, *LaB;
     double sf;
     double *LeA, *LeB;
 };
-__global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
+template <typename T> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;
     const long row = (long)blockIdx.x * p.N;
-    const FrInRow in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
+    const FrInRow<T> in{(const T *)p.LcA + row, (const T *)p.LcB + row, (const T *)p.LcW + row, (const T *)p.LcY + row,
+                        p.LaA + row, p.LaB + row};
     int pos[FR_J];
-    FrRowRaw raw[FR_J];
+    FrRowRaw<T> raw[FR_J];
 #pragma unroll
     for (int j = 0; j < FR_J; ++j) {
         const int i = threadIdx.x + j * FR_BLOCK;

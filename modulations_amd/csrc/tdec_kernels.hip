@@ -64,10 +64,15 @@ constexpr double LM_LN2 = 0x1.62e42fefa39efp-1;   // ln 2: bits -> nats
 // a branch of input class c (A^B) and parity pair wy carries +-U_c + v(wy),
 // v = {V0, V1, -V1, -V0}, so a parallel pair's log-sum is v(wy) + max*(U_c, -U_c)
 // (2 max* per step instead of 8; see pair_jac).
+// The parities w, y arrive as f64 here: an f32 channel LLR widened exactly (the
+// reference's numba promotes f32 * 0.5 to f64), or the caller's own f64 value
+// when bcjr_max_log_map is given float64 channel LLRs (numba's f64
+// specialisation of the same source: every sum is then f64 from unrounded
+// inputs).  The f32 overload below is the same operations.
 template <int ALGO = 0>
-__device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w, float y, float (&g)[8]) {
+__device__ __forceinline__ void gamma_from_sums(double inA, double inB, double w, double y, float (&g)[8]) {
     constexpr double hw = ALGO ? LM_K : 0.5;
-    const double hA = inA * hw, hB = inB * hw, hW = (double)w * hw, hY = (double)y * hw;
+    const double hA = inA * hw, hB = inB * hw, hW = w * hw, hY = y * hw;
     if constexpr (ALGO == 1) {
         g[0] = (float)(hA + hB);
         g[1] = (float)(hA + (-hB));
@@ -85,6 +90,10 @@ __device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w,
             g[bB * 4 + bW * 2 + 0] = (float)(l2 + hY);
             g[bB * 4 + bW * 2 + 1] = (float)(l2 + (-hY));
         }
+}
+template <int ALGO = 0>
+__device__ __forceinline__ void gamma_from_sums(double inA, double inB, float w, float y, float (&g)[8]) {
+    gamma_from_sums<ALGO>(inA, inB, (double)w, (double)y, g);
 }
 
 template <int ALGO = 0>
@@ -655,6 +664,31 @@ struct RowIn {
     }
     template <int ALGO> __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
         make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
+    }
+};
+
+// The same rows with float64 channel LLRs (numba's f64 specialisation of
+// :116-281): the sums inA = Lc_A + La_A, inB are formed at the load, in f64
+// from the unrounded values (:135-136), into the l slot, and the f64 parities
+// travel bit for bit in the 16 B of the v slot (W in .x/.y, Y in .z/.w).  The
+// siso<> code hands v.x / v.y only to the output's store, which RowOut ignores.
+struct RowIn64 {
+    const double *A, *B, *W, *Y;
+    const double *LaA, *LaB;
+    __device__ __forceinline__ Raw load(int k) const {
+        Raw r;
+        const double w = W[k], y = Y[k];
+        r.v = make_float4(__int_as_float(__double2loint(w)), __int_as_float(__double2hiint(w)),
+                          __int_as_float(__double2loint(y)), __int_as_float(__double2hiint(y)));
+        r.l = make_double2(A[k] + LaA[k], B[k] + LaB[k]);
+        return r;
+    }
+    template <int ALGO> __device__ __forceinline__ void gamma(const Raw &r, float (&g)[8], double &iA, double &iB) const {
+        iA = r.l.x;
+        iB = r.l.y;
+        const double w = __hiloint2double(__float_as_int(r.v.y), __float_as_int(r.v.x));
+        const double y = __hiloint2double(__float_as_int(r.v.w), __float_as_int(r.v.z));
+        gamma_from_sums<ALGO>(iA, iB, w, y, g);
     }
 };
 
@@ -1890,6 +1924,7 @@ __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_
 }
 
 // One SISO over B codewords given as [B][N] rows (the bcjr_max_log_map boundary).
+// Channel LLRs as float32 (Lc*) or, for the F64 kernels, float64 (Lc64*).
 struct SisoArgs {
     int B, N, n_waves;
     const float *LcA, *LcB, *LcW, *LcY;
@@ -1898,9 +1933,10 @@ struct SisoArgs {
     double *LeA, *LeB;
     float4 *ck;
     long ck_stride;
+    const double *Lc64A, *Lc64B, *Lc64W, *Lc64Y;
 };
 
-template <int ALGO, bool RAG> __device__ __forceinline__ void siso_rows(const SisoArgs &p) {
+template <int ALGO, bool RAG, bool F64> __device__ __forceinline__ void siso_rows(const SisoArgs &p) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
     if (wave >= p.n_waves) return;
@@ -1908,18 +1944,23 @@ template <int ALGO, bool RAG> __device__ __forceinline__ void siso_rows(const Si
     const long row = (cw < p.B ? cw : p.B - 1) * p.N;     // idle lanes recompute the last row, store nothing
     const int nw = (p.N + WIN - 1) / WIN;
     float4 *ck = p.ck + (long)wave * p.ck_stride;
-    RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
-    siso<ALGO, WIN, RAG>(in, RowOut{p.LeA + row, p.LeB + row, cw < p.B}, p.N, ck, ck + (long)nw * 4 * WAVE, WAVE,
-                         lane, p.sf);
+    const RowOut out{p.LeA + row, p.LeB + row, cw < p.B};
+    if constexpr (F64) {
+        RowIn64 in{p.Lc64A + row, p.Lc64B + row, p.Lc64W + row, p.Lc64Y + row, p.LaA + row, p.LaB + row};
+        siso<ALGO, WIN, RAG>(in, out, p.N, ck, ck + (long)nw * 4 * WAVE, WAVE, lane, p.sf);
+    } else {
+        RowIn in{p.LcA + row, p.LcB + row, p.LcW + row, p.LcY + row, p.LaA + row, p.LaB + row};
+        siso<ALGO, WIN, RAG>(in, out, p.N, ck, ck + (long)nw * 4 * WAVE, WAVE, lane, p.sf);
+    }
 }
-template <bool RAG>
+template <bool RAG, bool F64 = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void k_siso_batch(SisoArgs p) {
-    siso_rows<0, RAG>(p);
+    siso_rows<0, RAG, F64>(p);
 }
-template <bool RAG>
+template <bool RAG, bool F64 = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_siso_batch_logmap(
     SisoArgs p) {
-    siso_rows<1, RAG>(p);
+    siso_rows<1, RAG, F64>(p);
 }
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.

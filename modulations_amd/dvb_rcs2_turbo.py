@@ -69,6 +69,25 @@ class _Handle:
         self.llr_len = _n.lib().tdec_llr_len(h)
         self.enc_len = _n.lib().tdec_encoded_len(h)
         self.lock = threading.Lock()
+        L = _n.lib()
+        self.siso_staged = getattr(L, "tdec_siso_staged", None)
+        self.n = n
+        self._views = None
+
+    def siso_views(self):
+        """(float32-Lc views, float64-Lc views) of the handle's single-row SISO
+        staging: 8 numpy arrays of N each (LcA, LcB, LcW, LcY, LaA, LaB, LeA, LeB)
+        over the page-locked buffer of tdec_siso_staging (include/tdec.h)."""
+        v = self._views
+        if v is None:
+            buf, sl = C.c_void_p(), C.c_size_t()
+            self.call("tdec_siso_staging", 1, C.byref(buf), C.byref(sl))
+            sl, n = sl.value, self.n
+            raw = np.frombuffer((C.c_char * (8 * sl)).from_address(buf.value), np.uint8)
+            f64 = [raw[i * sl:i * sl + 8 * n].view(np.float64) for i in range(8)]
+            f32 = [raw[i * sl:i * sl + 4 * n].view(np.float32) for i in range(4)] + f64[4:]
+            v = self._views = (f32, f64)
+        return v
 
     def call(self, name, *args):
         """lib().<name>(self.h, *args) under the handle lock, errors raised."""
@@ -88,11 +107,14 @@ class _Handle:
 
 
 def _default_device():
+    """torch's current device when torch has initialised its GPU state, else 0.
+    Cheap enough for every call (no import, no device query before that): the
+    per-call functions resolve it each time."""
+    t = sys.modules.get("torch")
     try:
-        import torch
-        if torch.cuda.is_available():
-            return torch.cuda.current_device()
-    except Exception:  # pragma: no cover - torch is optional for the host API
+        if t is not None and t.cuda.is_initialized():
+            return t.cuda.current_device()
+    except Exception:  # pragma: no cover - a torch without a usable cuda module
         pass
     return 0
 
@@ -372,20 +394,95 @@ def pinned_empty(shape, dtype=np.float32):
 
 _SISO_CACHE = {}
 _CACHE_LOCK = threading.Lock()
+_F32 = np.dtype(np.float32)
+_F64 = np.dtype(np.float64)
+
+
+def _tables_key(tabs):
+    """Bytes identifying the five trellis tables (the handle cache key).  The
+    usual call passes the codec's own int32 [16, 4] arrays: their bytes directly;
+    anything else goes through packed_tables' conversion."""
+    if all(type(t) is np.ndarray and t.dtype == np.int32 and t.size == 64 and t.flags.c_contiguous for t in tabs):
+        return b"".join([t.tobytes() for t in tabs])
+    return _t.packed_tables(*tabs).tobytes()
+
+
+def _siso_handle(N, tkey, algo, dev):
+    key = (N, tkey, algo, dev)
+    h = _SISO_CACHE.get(key)
+    if h is None:
+        with _CACHE_LOCK:
+            h = _SISO_CACHE.get(key)
+            if h is None:
+                ident = np.arange(N, dtype=np.int32)
+                tabs = np.frombuffer(tkey, np.int32).reshape(5, 16, 4)
+                h = _SISO_CACHE[key] = _Handle(dev, N, PUNCTURE_PATTERNS['1/3'], 1, algo, ident, ident, tabs)
+    return h
+
+
+def _short(n, N):
+    return IndexError(f"index {n} is out of bounds for axis 0 with size {n}")
+
+
+def _siso_inputs(Lc, La, N, ndim):
+    """The SISO's inputs with numba's typing of bcjr_max_log_map (:116-160, :267):
+      * channel LLRs: four float32 arrays run the float32 specialisation (each use
+        widens them to f64: f64(Lc_A) + La_A, f64(par_W) * 0.5); float64 arrays
+        -- or a mix, or integer / bool arrays, which numba also widens to f64 --
+        run the float64 one, where those sums are formed from the unrounded
+        values.  Widening is exact, so a float32 array in a mixed call gives the
+        values numba uses.
+      * a-priori: float64 only.  With float32 La the reference sums in_A = Lc_A +
+        La_A in float32 and builds the branch metrics from a float32 m, which the
+        shim that pins every fixture cannot reproduce (numpy 2 keeps 0.0 + f32 in
+        float32 where numba promotes to f64), so that call is refused, not guessed.
+    Returns (f64, [A, B, W, Y], [LaA, LaB]): the caller's arrays (not copied),
+    each checked to be ndim-D with at least N entries along its last axis."""
+    lc = [x if type(x) is np.ndarray else np.asarray(x) for x in Lc]
+    la = [x if type(x) is np.ndarray else np.asarray(x) for x in La]
+    for x in la:
+        if x.dtype is not _F64 and x.dtype != _F64:
+            raise TypeError(f"bcjr_max_log_map: a-priori LLRs must be float64 (got {x.dtype}); the reference's "
+                            "float32 a-priori arithmetic is not reproducible here (parity unpinned)")
+    f64 = False
+    for x in lc:
+        if x.dtype is not _F32 and x.dtype != _F32:
+            if x.dtype.kind not in "fiub" or x.dtype.itemsize > 8 or x.dtype == np.float16:
+                raise TypeError(f"bcjr_max_log_map: channel LLRs must be float32 or float64 arrays (got {x.dtype})")
+            f64 = True
+    for x in lc + la:
+        if x.ndim != ndim:
+            raise ValueError(f"bcjr_max_log_map{'_batch' if ndim == 2 else ''} takes {ndim}-D arrays")
+        if x.shape[-1] < N:
+            raise _short(x.shape[-1], N)
+    return f64, lc, la
 
 
 def bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,
                      scaling_factor):
     """Max-Log-MAP SISO (reference :116-281), one codeword, on the GPU.
 
-    Same arguments and outputs: f32 channel LLRs, f64 a-priori, the five int32
+    Same arguments and outputs: channel LLRs (float32, or float64 -- numba's
+    float64 specialisation, reproduced), float64 a-priori, the five int32
     [16,4] trellis tables, N couples and the extrinsic scaling factor; returns
     freshly allocated (Le_A, Le_B) f64 arrays.  Inputs are not mutated.
+
+    Per call: the inputs are copied into the handle's page-locked staging
+    (tdec_siso_staging) and one argument-free C call runs the SISO there.
     """
-    LeA, LeB = bcjr_max_log_map_batch(np.asarray(Lc_A)[None], np.asarray(Lc_B)[None], np.asarray(Lc_W)[None],
-                                      np.asarray(Lc_Y)[None], np.asarray(La_A)[None], np.asarray(La_B)[None],
-                                      next_st, out_W, out_Y, prev_st, prev_inp, N, scaling_factor)
-    return LeA[0], LeB[0]
+    N = int(N)
+    f64, lc, la = _siso_inputs((Lc_A, Lc_B, Lc_W, Lc_Y), (La_A, La_B), N, 1)
+    if N == 0:   # the reference's recursions run over range(0): empty extrinsics
+        return np.zeros(0), np.zeros(0)
+    h = _siso_handle(N, _tables_key((next_st, out_W, out_Y, prev_st, prev_inp)), 0, _default_device())
+    v = h.siso_views()[f64]
+    with h.lock:
+        for d, x in zip(v, lc + la):
+            np.copyto(d, x if x.shape[0] == N else x[:N])
+        rc = h.siso_staged(h.h, 1, f64, float(scaling_factor))
+        if rc:
+            _n.check(rc)
+        return v[6].copy(), v[7].copy()
 
 
 bcjr_decode_circular = bcjr_max_log_map   # historic name of the same SISO (SURVEY §0 fact 2)
@@ -393,29 +490,25 @@ bcjr_decode_circular = bcjr_max_log_map   # historic name of the same SISO (SURV
 
 def bcjr_max_log_map_batch(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,
                            scaling_factor, algo="max-log", device=None):
-    """bcjr_max_log_map over B codewords at once: [B, N] arrays in, (Le_A, Le_B) [B, N] out."""
+    """bcjr_max_log_map over B codewords at once: [B, N] arrays in, (Le_A, Le_B) [B, N] out
+    (channel LLRs float32 or float64 as in bcjr_max_log_map)."""
     N = int(N)
-    f32 = lambda x: np.ascontiguousarray(np.asarray(x, np.float32)[:, :N])
-    f64 = lambda x: np.ascontiguousarray(np.asarray(x, np.float64)[:, :N])
-    A, Bv, W, Y, la, lb = f32(Lc_A), f32(Lc_B), f32(Lc_W), f32(Lc_Y), f64(La_A), f64(La_B)
-    for x in (A, Bv, W, Y, la, lb):
-        if x.shape[1] < N:
-            raise IndexError(f"index {x.shape[1]} is out of bounds for axis 0 with size {x.shape[1]}")
-    tabs = _t.packed_tables(next_st, out_W, out_Y, prev_st, prev_inp)
-    if N == 0:   # the reference's recursions run over range(0): empty extrinsics
+    f64, lc, la = _siso_inputs((Lc_A, Lc_B, Lc_W, Lc_Y), (La_A, La_B), N, 2)
+    dt = _F64 if f64 else _F32
+    A, Bv, W, Y = (np.ascontiguousarray(x[:, :N], dt) for x in lc)
+    la, lb = (np.ascontiguousarray(x[:, :N], _F64) for x in la)
+    if any(x.shape[0] != A.shape[0] for x in (A, Bv, W, Y, la, lb)):
+        raise ValueError("bcjr_max_log_map_batch takes [B, N] arrays of one batch size")
+    if N == 0:
         return np.zeros((A.shape[0], 0)), np.zeros((A.shape[0], 0))
-    dev = _default_device() if device is None else device
-    key = (N, tabs.tobytes(), ALGOS[algo] if isinstance(algo, str) else int(algo), dev)
-    with _CACHE_LOCK:
-        h = _SISO_CACHE.get(key)
-        if h is None:
-            ident = np.arange(N, dtype=np.int32)
-            h = _SISO_CACHE[key] = _Handle(dev, N, PUNCTURE_PATTERNS['1/3'], 1, key[2], ident, ident, tabs)
+    algo = ALGOS[algo] if isinstance(algo, str) else int(algo)
+    h = _siso_handle(N, _tables_key((next_st, out_W, out_Y, prev_st, prev_inp)), algo,
+                     _default_device() if device is None else device)
     B = A.shape[0]
     LeA = np.zeros((B, N))
     LeB = np.zeros((B, N))
-    h.call("tdec_siso_batch", B, _n.ptr(A), _n.ptr(Bv), _n.ptr(W), _n.ptr(Y), _n.ptr(la), _n.ptr(lb),
-           float(scaling_factor), _n.ptr(LeA), _n.ptr(LeB))
+    h.call("tdec_siso_batch_f64" if f64 else "tdec_siso_batch", B, A.ctypes.data, Bv.ctypes.data, W.ctypes.data,
+           Y.ctypes.data, la.ctypes.data, lb.ctypes.data, float(scaling_factor), LeA.ctypes.data, LeB.ctypes.data)
     return LeA, LeB
 
 

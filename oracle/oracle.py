@@ -36,6 +36,8 @@ def lib():
         L.orc_interleaver.argtypes = [C.c_int, _i32p, _i32p, _i32p]
         L.orc_siso.argtypes = [C.c_int, _f32p, _f32p, _f32p, _f32p, _f64p, _f64p, _i32p,
                                C.c_double, C.c_int, _f64p, _f64p]
+        L.orc_siso64.argtypes = [C.c_int, _f64p, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p,
+                                 C.c_double, C.c_int, _f64p, _f64p]
         L.orc_decode.argtypes = [C.c_int, C.c_int, _u8p, C.c_int, C.c_int, _i32p, _i32p, _i32p,
                                  _f32p, C.c_long, _i32p, C.c_void_p]
         L.orc_decode.restype = C.c_int
@@ -91,12 +93,21 @@ def interleaver(n, params):
 
 
 def siso(LcA, LcB, LcW, LcY, LaA, LaB, tables, sf, algo=0):
+    """bcjr_max_log_map (dvb_rcs2_turbo.py:116-281).  The channel LLRs keep numba's
+    typing: four float32 arrays run the f32 specialisation, anything else (float64,
+    integers, a mix) the float64 one -- every use widens Lc to f64 first, so the
+    values widened exactly give the same results (the product's dispatch rule)."""
     n = len(LcA)
     c = lambda x, dt: np.ascontiguousarray(x, dt)
     LeA = np.zeros(n)
     LeB = np.zeros(n)
-    lib().orc_siso(n, c(LcA, np.float32), c(LcB, np.float32), c(LcW, np.float32), c(LcY, np.float32),
-                   c(LaA, np.float64), c(LaB, np.float64), c(tables, np.int32), float(sf), algo, LeA, LeB)
+    lc = [np.asarray(x) for x in (LcA, LcB, LcW, LcY)]
+    if all(x.dtype == np.float32 for x in lc):
+        lib().orc_siso(n, *(c(x, np.float32) for x in lc), c(LaA, np.float64), c(LaB, np.float64),
+                       c(tables, np.int32), float(sf), algo, LeA, LeB)
+    else:
+        lib().orc_siso64(n, *(c(x, np.float64) for x in lc), c(LaA, np.float64), c(LaB, np.float64),
+                         c(tables, np.int32), float(sf), algo, LeA, LeB)
     return LeA, LeB
 
 

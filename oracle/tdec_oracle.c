@@ -11,7 +11,7 @@
  *
  *   orc_trellis          dvb_rcs2_turbo.py:327-396  (_init_trellis)
  *   orc_interleaver      dvb_rcs2_turbo.py:311-325  (_init_interleaver; inverse = stable argsort, see below)
- *   orc_siso             dvb_rcs2_turbo.py:116-281  (bcjr_max_log_map)  + build-defined log-MAP
+ *   orc_siso / orc_siso64 dvb_rcs2_turbo.py:116-281 (bcjr_max_log_map; f32 / f64 channel LLRs) + build-defined log-MAP
  *   orc_decode           dvb_rcs2_turbo.py:464-537  (DVBRCS2_Turbo.decode)
  *   orc_encode           dvb_rcs2_turbo.py:37-114, 404-462 (GF(2) helpers, _encode_component, encode)
  *   orc_demap_c64/_c128  test_sdr_with_coding.py:200-225 (compute_llr) + numpy's complex |.|
@@ -197,9 +197,21 @@ static inline float lse4(float x0, float x1, float x2, float x3)
 float orc_jac(float a, float b) { return jac(a, b); }   /* exported for the accuracy tests (bits) */
 float orc_lse4(float a, float b, float c, float d) { return lse4(a, b, c, d); }
 
-static void siso_exact(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
-                       const double *LaA, const double *LaB, const int32_t *tables, double sf,
-                       double *LeA, double *LeB);
+/* Channel LLRs as numba sees them: float32 arrays (every use widens them to
+ * f64 first: `Lc_A[k] + La_A[k]`, `par_W * 0.5` promote) or float64 arrays
+ * (numba's f64 specialisation of the same source, :135-160 / :267-268: the
+ * same f64 operations on the unrounded values).  An f32 value widened is exact,
+ * so one restatement over f64 inputs serves both. */
+typedef struct { const void *p[4]; int f64; } lc_in;
+static inline double LC(const lc_in *c, int i, int k)
+{
+    return c->f64 ? ((const double *)c->p[i])[k] : (double)((const float *)c->p[i])[k];
+}
+
+static void siso_exact(int N, const lc_in *lc, const double *LaA, const double *LaB, const int32_t *tables,
+                       double sf, double *LeA, double *LeB);
+static void siso_core(int N, const lc_in *lc, const double *LaA, const double *LaB, const int32_t *tables,
+                      double sf, int algo, double *LeA, double *LeB);
 
 /* bcjr_max_log_map, dvb_rcs2_turbo.py:116-281 (algo 0); algo 1 = the build's
  * log-MAP (above): same passes, metrics in bits, max -> max*; algo 2 = exact
@@ -208,7 +220,24 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
               const double *LaA, const double *LaB, const int32_t *tables, double sf, int algo,
               double *LeA, double *LeB)
 {
-    if (algo == 2) { siso_exact(N, LcA, LcB, LcW, LcY, LaA, LaB, tables, sf, LeA, LeB); return; }
+    const lc_in lc = {{LcA, LcB, LcW, LcY}, 0};
+    if (algo == 2) siso_exact(N, &lc, LaA, LaB, tables, sf, LeA, LeB);
+    else siso_core(N, &lc, LaA, LaB, tables, sf, algo, LeA, LeB);
+}
+
+/* The same with float64 channel LLRs (numba's float64 specialisation). */
+void orc_siso64(int N, const double *LcA, const double *LcB, const double *LcW, const double *LcY,
+                const double *LaA, const double *LaB, const int32_t *tables, double sf, int algo,
+                double *LeA, double *LeB)
+{
+    const lc_in lc = {{LcA, LcB, LcW, LcY}, 1};
+    if (algo == 2) siso_exact(N, &lc, LaA, LaB, tables, sf, LeA, LeB);
+    else siso_core(N, &lc, LaA, LaB, tables, sf, algo, LeA, LeB);
+}
+
+static void siso_core(int N, const lc_in *lc, const double *LaA, const double *LaB, const int32_t *tables,
+                      double sf, int algo, double *LeA, double *LeB)
+{
     const int32_t *nx = tables, *ow = tables + 64, *oy = tables + 128, *ps = tables + 192, *pi = tables + 256;
     float *gamma = (float *)calloc((size_t)N * NS * 4, sizeof(float));
     float *alpha = (float *)calloc((size_t)(N + 1) * NS, sizeof(float));
@@ -218,11 +247,11 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
 
     /* 1. gamma (:127-160): f64 sum in fixed order, stored as f32 */
     for (int k = 0; k < N; ++k) {
-        double in_A = (double)LcA[k] + LaA[k];
-        double in_B = (double)LcB[k] + LaB[k];
-        float par_W = LcW[k], par_Y = LcY[k];
+        double in_A = LC(lc, 0, k) + LaA[k];
+        double in_B = LC(lc, 1, k) + LaB[k];
+        double par_W = LC(lc, 2, k), par_Y = LC(lc, 3, k);
         if (algo) {   /* log-MAP branch halves (round 4): f64 sums rounded once */
-            const double hA = in_A * hw, hB = in_B * hw, hW = (double)par_W * hw, hY = (double)par_Y * hw;
+            const double hA = in_A * hw, hB = in_B * hw, hW = par_W * hw, hY = par_Y * hw;
             UV[4 * k + 0] = (float)(hA + hB);
             UV[4 * k + 1] = (float)(hA + (-hB));
             UV[4 * k + 2] = (float)(hW + hY);
@@ -235,8 +264,8 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
                 double m = 0.0;
                 m += in_A * (bA == 0 ? hw : -hw);
                 m += in_B * (bB == 0 ? hw : -hw);
-                m += (double)par_W * (bW == 0 ? hw : -hw);
-                m += (double)par_Y * (bY == 0 ? hw : -hw);
+                m += par_W * (bW == 0 ? hw : -hw);
+                m += par_Y * (bY == 0 ? hw : -hw);
                 gamma[((size_t)k * NS + s) * 4 + inp] = (float)m;
             }
     }
@@ -343,8 +372,8 @@ void orc_siso(int N, const float *LcA, const float *LcB, const float *LcW, const
             LpB = pB0 - pB1;
         }
         /* log-MAP: bits -> nats by one f64 multiply */
-        double a = (algo ? (double)LpA * LM_LN2 : (double)LpA) - ((double)LcA[k] + LaA[k]);
-        double b = (algo ? (double)LpB * LM_LN2 : (double)LpB) - ((double)LcB[k] + LaB[k]);
+        double a = (algo ? (double)LpA * LM_LN2 : (double)LpA) - (LC(lc, 0, k) + LaA[k]);
+        double b = (algo ? (double)LpB * LM_LN2 : (double)LpB) - (LC(lc, 1, k) + LaB[k]);
         a *= sf; b *= sf;
         const double limit = 300.0;
         if (a > limit) a = limit;
@@ -380,9 +409,8 @@ static inline double jac64(double a, double b)
     return m + log1p(exp(-d));
 }
 
-static void siso_exact(int N, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
-                       const double *LaA, const double *LaB, const int32_t *tables, double sf,
-                       double *LeA, double *LeB)
+static void siso_exact(int N, const lc_in *lc, const double *LaA, const double *LaB, const int32_t *tables,
+                       double sf, double *LeA, double *LeB)
 {
     const int32_t *nx = tables, *ow = tables + 64, *oy = tables + 128, *ps = tables + 192, *pi = tables + 256;
     double *gamma = (double *)calloc((size_t)N * NS * 4, sizeof(double));
@@ -392,12 +420,12 @@ static void siso_exact(int N, const float *LcA, const float *LcB, const float *L
 #define ALP(k, s) alpha[(size_t)(k) * NS + (s)]
 #define BET(k, s) beta[(size_t)(k) * NS + (s)]
     for (int k = 0; k < N; ++k) {
-        const double in_A = (double)LcA[k] + LaA[k], in_B = (double)LcB[k] + LaB[k];
+        const double in_A = LC(lc, 0, k) + LaA[k], in_B = LC(lc, 1, k) + LaB[k];
+        const double W = LC(lc, 2, k), Y = LC(lc, 3, k);
         for (int s = 0; s < NS; ++s)
             for (int inp = 0; inp < 4; ++inp) {
                 int bA = (inp >> 1) & 1, bB = inp & 1, bW = ow[s * 4 + inp], bY = oy[s * 4 + inp];
-                GAM(k, s, inp) = 0.5 * ((bA ? -in_A : in_A) + (bB ? -in_B : in_B) + (bW ? -(double)LcW[k] : (double)LcW[k]) +
-                                        (bY ? -(double)LcY[k] : (double)LcY[k]));
+                GAM(k, s, inp) = 0.5 * ((bA ? -in_A : in_A) + (bB ? -in_B : in_B) + (bW ? -W : W) + (bY ? -Y : Y));
             }
     }
     for (int pass = 0; pass < 2; ++pass) {
@@ -430,8 +458,8 @@ static void siso_exact(int N, const float *LcA, const float *LcB, const float *L
         double app[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
         for (int s = 0; s < NS; ++s)
             for (int inp = 0; inp < 4; ++inp) app[inp] = jac64(app[inp], ALP(k, s) + GAM(k, s, inp) + BET(k + 1, nx[s * 4 + inp]));
-        double a = (jac64(app[0], app[1]) - jac64(app[2], app[3])) - ((double)LcA[k] + LaA[k]);
-        double b = (jac64(app[0], app[2]) - jac64(app[1], app[3])) - ((double)LcB[k] + LaB[k]);
+        double a = (jac64(app[0], app[1]) - jac64(app[2], app[3])) - (LC(lc, 0, k) + LaA[k]);
+        double b = (jac64(app[0], app[2]) - jac64(app[1], app[3])) - (LC(lc, 1, k) + LaB[k]);
         a *= sf; b *= sf;
         if (a > 300.0) a = 300.0;
         if (a < -300.0) a = -300.0;

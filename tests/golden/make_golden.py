@@ -133,6 +133,66 @@ def gen_siso(T):
     np.savez_compressed(os.path.join(OUT, "siso.npz"), **out)
 
 
+def gen_siso_f64(T):
+    """bcjr_max_log_map with FLOAT64 channel LLRs: numba
+    specialises the same source for f64 Lc, so in_A = Lc_A + La_A and the parity
+    terms are formed from the unrounded values (:135-160) and the extrinsic
+    subtracts the f64 sum (:267-268).  All-f64 arithmetic is the same under numba
+    and CPython + numpy, so the shim pins it.  Also: a mixed call (f64 A / W, f32
+    B / Y: numba widens the f32 ones, numpy does too in every sum that has an f64
+    operand) and integer channel LLRs (int64 + f64 -> f64 in both).  Rows per N:
+    random scales, values f32 cannot hold (1e-310 denormals, 1e39, 0.1 + 1e-12),
+    NaN / +-inf, sf 0.7 and 1.0."""
+    rng = np.random.default_rng(64)
+    c = make_codec(T, 48, "1/3")
+    tabs = (c.next_state, c.out_W, c.out_Y, c.prev_state, c.prev_input)
+    out = {}
+    for n, count in ((48, 12), (212, 8), (752, 6)):
+        rows = []
+        for i in range(count):
+            sc = [0.3, 2.0, 9.0, 40.0][i % 4]
+            la_sc = [0.0, 4.0, 25.0, 80.0][(i // 2) % 4]
+            Lc = rng.standard_normal((4, n)) * sc
+            La = rng.standard_normal((2, n)) * la_sc
+            kind = i % 6
+            if kind == 1:   # just off the f32 grid: every value differs from its f32 rounding
+                Lc = Lc + 1e-9 * rng.standard_normal((4, n))
+            elif kind == 2:   # f64-only magnitudes: denormals and values beyond f32's range
+                pos = rng.integers(0, n, max(3, n // 8))
+                Lc[2, pos] = 1e-310 * rng.standard_normal(len(pos))
+                Lc[3, pos[::2]] = 3e39 * np.sign(rng.standard_normal(len(pos[::2])))
+                Lc[0, pos[1::3]] = -4e-320
+            elif kind == 3:   # non-finite channel values
+                pos = rng.integers(0, n, max(2, n // 16))
+                Lc[rng.integers(0, 4), pos] = np.nan
+                Lc[rng.integers(0, 4), pos[::2]] = np.inf
+                Lc[1, pos[1::2]] = -np.inf
+            elif kind == 4:   # saturating extrinsics (+-300 clip)
+                Lc *= 150.0
+                La *= 10.0
+            sf = 0.7 if i % 3 else 1.0
+            a, b = T.bcjr_max_log_map(Lc[0], Lc[1], Lc[2], Lc[3], La[0], La[1], *tabs, n, sf)
+            rows.append((Lc, La, sf, a, b))
+        out[f"Lc_{n}"] = np.stack([r[0] for r in rows])          # [count, 4, n] float64
+        out[f"La_{n}"] = np.stack([r[1] for r in rows])          # [count, 2, n] float64
+        out[f"sf_{n}"] = np.array([r[2] for r in rows])
+        out[f"LeA_{n}"] = np.stack([r[3] for r in rows])
+        out[f"LeB_{n}"] = np.stack([r[4] for r in rows])
+        print(f"  siso_f64 N={n}", flush=True)
+    # a mixed-dtype call and an integer-Lc call per N (N = 48, 212)
+    for n in (48, 212):
+        Lc = rng.standard_normal((4, n)) * 5.0 + 1e-7
+        La = rng.standard_normal((2, n)) * 12.0
+        A, B, W, Y = Lc[0], Lc[1].astype(np.float32), Lc[2], Lc[3].astype(np.float32)
+        a, b = T.bcjr_max_log_map(A, B, W, Y, La[0], La[1], *tabs, n, 0.7)
+        out.update({f"mix_A_{n}": A, f"mix_B_{n}": B, f"mix_W_{n}": W, f"mix_Y_{n}": Y, f"mix_La_{n}": La,
+                    f"mix_LeA_{n}": a, f"mix_LeB_{n}": b})
+        I = rng.integers(-40, 41, (4, n)).astype(np.int64)
+        a, b = T.bcjr_max_log_map(I[0], I[1], I[2], I[3], La[0], La[1], *tabs, n, 1.0)
+        out.update({f"int_Lc_{n}": I, f"int_La_{n}": La, f"int_LeA_{n}": a, f"int_LeB_{n}": b})
+    np.savez_compressed(os.path.join(OUT, "siso_f64.npz"), **out)
+
+
 class _Capture:
     """Wrap T.bcjr_max_log_map (resolved as a module global at call time by
     DVBRCS2_Turbo.decode, dvb_rcs2_turbo.py:499/515) to record SISO I/O."""

@@ -4,7 +4,10 @@ persistent tile loop wraps), where the oracle cannot check every codeword:
 
 * determinism, batch-order invariance and shard equivalence (one launch ==
   the concatenation of launches over its shards) -- bit for bit;
-* oracle spot checks on first / middle / last codewords of a large batch;
+* the timed kernel itself (k_turbo_decode: batches above the small-batch
+  decoders' limit) against the oracle on 4 096 rows of each full-size batch --
+  the first 2 048 (32 tiles) and 2 048 spread over the whole batch, so rows of
+  every round of the persistent tile loop are checked -- bits AND L_final;
 * the fused demap+decode pipeline == compute_llr -> float32 -> decode;
 * with a true permutation (valid-perm mode) a noise-free batch decodes to its
   info bits exactly (encode -> decode round trip).
@@ -28,10 +31,37 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _oracle_bits(codec, llr_rows):
+def _oracle_bits(codec, llr_rows, want_lfinal=False):
     t, _ = O.trellis()
     return O.decode_batch(llr_rows, codec.N, codec.punct["period"], T.puncture_matrix(codec.punct),
-                          codec.iterations, codec.perm, codec.inv_perm, t)
+                          codec.iterations, codec.perm, codec.inv_perm, t, nthreads=16, want_lfinal=want_lfinal)
+
+
+def _host_llr_rows(codec, syms_rows, mod, n0):
+    """compute_llr (the C oracle's restatement) -> decoder sign -> float32, per row."""
+    cons = D.constellation(mod)
+    bps = D.MODULATIONS[mod]["bps"]
+    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
+    R, S = syms_rows.shape
+    llr = -O.demap(np.ascontiguousarray(syms_rows).reshape(-1), cons, bps, nve, div_f32=div32)
+    return np.ascontiguousarray(llr.reshape(R, S * bps)[:, :codec.n_coded]).astype(np.float32)
+
+
+def _check_throughput_kernel_vs_oracle(codec, pipe, syms, B, n0, mod):
+    """Re-decode the pipeline's planes (B > the small-batch limit, so
+    k_turbo_decode runs) with L_final and compare 4 096 rows with the oracle."""
+    lf = torch.empty((B, codec.k_info), dtype=torch.float64, device=syms.device)
+    bits = torch.empty((B, codec.k_info), dtype=torch.int32, device=syms.device)
+    codec.decode_planes_device(pipe.planes, B, bits, lfinal=lf)
+    torch.cuda.synchronize()
+    idx = np.unique(np.concatenate([np.arange(2048), np.linspace(2048, B - 1, 2048).astype(np.int64)]))
+    assert len(idx) >= 4096 and idx[-1] == B - 1
+    ti = torch.as_tensor(idx, device=syms.device)
+    llr = _host_llr_rows(codec, syms[ti].cpu().numpy(), mod, n0)
+    rb, rl = _oracle_bits(codec, llr, want_lfinal=True)
+    assert np.array_equal(bits[ti].cpu().numpy(), rb)
+    np.testing.assert_array_equal(lf[ti].cpu().numpy(), rl)
+    return bits
 
 
 def test_full_size_pipeline_properties():
@@ -52,20 +82,17 @@ def test_full_size_pipeline_properties():
     bb = p2.run(syms[h:].contiguous(), n0).clone()
     torch.cuda.synchronize()
     assert torch.equal(torch.cat([ba, bb]), b1)
-    # batch-order invariance
-    perm = torch.randperm(4096, device=dev)
-    pp = DevicePipeline(codec, "16QAM", 4096, dev)
-    bp = pp.run(syms[:4096][perm].contiguous(), n0)
+    # the timed kernel against the oracle: 4 096 rows, bits and L_final
+    bt = _check_throughput_kernel_vs_oracle(codec, pipe, syms, B, n0, "16QAM")
+    assert torch.equal(bt, b1)
+    # batch-order invariance of the throughput kernel (16 384 > the small-batch limit)
+    perm = torch.randperm(16384, device=dev)
+    pp = DevicePipeline(codec, "16QAM", 16384, dev)
+    bp = pp.run(syms[:16384][perm].contiguous(), n0)
     torch.cuda.synchronize()
-    assert torch.equal(bp, b1[:4096][perm])
-    # oracle spot checks: first, middle, last codewords
-    cons = D.constellation("16QAM")
-    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
-    idx = [0, 1, 63, 64, B // 2, B - 65, B - 1]
-    rows = syms[idx].cpu().numpy()
-    llr = np.stack([-O.demap(r, cons, 4, nve, div_f32=div32)[:codec.n_coded] for r in rows]).astype(np.float32)
-    assert np.array_equal(b1[idx].cpu().numpy(), _oracle_bits(codec, llr))
-    # fused pipeline == compute_llr_device -> f32 -> decode_device on the same symbols
+    assert torch.equal(bp, b1[:16384][perm])
+    # cross-decoder: the frame decoder (a 2 048-row call) gives the throughput
+    # kernel's bits; the fused pipeline == compute_llr_device -> f32 -> decode_device
     llr_dev = D.compute_llr_device(syms[:2048].contiguous(), "16QAM", np.float64(n0), sign=-1)
     llr32 = llr_dev.view(2048, -1)[:, :codec.n_coded].to(torch.float32).contiguous()
     bd = codec.decode_device(llr32)
@@ -122,10 +149,5 @@ def test_ragged_checkpoint_windows_full_size(n, mod):
     b2 = pipe.run(syms, n0).clone()
     torch.cuda.synchronize()
     assert torch.equal(b1, b2)
-    cons = D.constellation(mod)
-    bps = D.MODULATIONS[mod]["bps"]
-    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
-    idx = [0, 64, 131_071, 131_072, B // 2, B - 1]
-    rows = syms[idx].cpu().numpy()
-    llr = np.stack([-O.demap(r, cons, bps, nve, div_f32=div32)[:codec.n_coded] for r in rows]).astype(np.float32)
-    assert np.array_equal(b1[idx].cpu().numpy(), _oracle_bits(codec, llr))
+    # the timed kernel against the oracle: 4 096 rows (incl. the last, ragged tile), bits and L_final
+    assert torch.equal(_check_throughput_kernel_vs_oracle(codec, pipe, syms, B, n0, mod), b1)

@@ -957,7 +957,11 @@ static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // p
 // LDS) takes the small batches when its LDS fits (N <= 805: every BASELINE
 // config); the round-3 state-per-lane decoder (tdec_lowlat.hip) otherwise, or
 // with TDEC_FRAME=0 (A/B).
-static bool frame_fits(int N, bool dec) { return N <= FR_J * FR_BLOCK && fr_lds(N, dec).total <= FR_LDS_MAX; }
+// The decoder keeps Le2 in global scratch where its full LDS plan does not fit (N > 805).
+static bool frame_le2_global(int N) { return fr_lds(N, true, false).total > FR_LDS_MAX; }
+static bool frame_fits(int N, bool dec) {
+    return N <= FR_J * FR_BLOCK && fr_lds(N, dec, dec && frame_le2_global(N)).total <= FR_LDS_MAX;
+}
 static bool use_frame_decoder(const tdec_t *h) {
     const char *e = getenv("TDEC_FRAME");   // read per call: tests switch decoders in-process
     return !(e && e[0] == '0') && frame_fits(h->N, true);
@@ -981,7 +985,9 @@ static bool lowlat_usable(const tdec_t *h) {
 // up to that minus 4): the frame decoder keeps only Le1 (N double2 per row) outside
 // LDS, the state-per-lane decoder three extrinsic planes and the alpha / beta stores.
 static int ll_cap_of(const tdec_t *h) {
-    if (use_frame_decoder(h)) return (int)std::min<size_t>(h->ll_ws.cap / ((size_t)h->N * sizeof(double2)), 1 << 30);
+    if (use_frame_decoder(h))   // Le1 (and with Le2 in global scratch, Le2) per row
+        return (int)std::min<size_t>(h->ll_ws.cap / ((frame_le2_global(h->N) ? 2 : 1) * (size_t)h->N * sizeof(double2)),
+                                     1 << 30);
     return (int)std::min(h->ll_ws.cap / (ll_ws_elems(h->N) * sizeof(double2)), h->ll_st.cap / (ll_st_elems(h->N) * sizeof(float)));
 }
 static bool use_lowlat(const tdec_t *h, int B) {
@@ -995,8 +1001,8 @@ static int frame_lds_attr(int device) {
     if (device < 0 || device >= 256) return fail(TDEC_EINVAL, "device ordinal out of range");
     std::lock_guard<std::mutex> lk(mu);
     if (done[device]) return 0;
-    const void *fns[] = {(const void *)k_turbo_decode_frame, (const void *)k_siso_frame<float>,
-                         (const void *)k_siso_frame<double>};
+    const void *fns[] = {(const void *)k_turbo_decode_frame<false>, (const void *)k_turbo_decode_frame<true>,
+                         (const void *)k_siso_frame<float>, (const void *)k_siso_frame<double>};
     for (const void *f : fns) {
         const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
         if (r != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(r));
@@ -1008,7 +1014,7 @@ static int frame_lds_attr(int device) {
 static int ensure_lowlat(tdec_t *h, int B) {
     if (B > lowlat_max(h) || B + 4 <= ll_cap_of(h) || !lowlat_usable(h)) return 0;
     const size_t cap = std::min(lowlat_max(h), std::max(B, 64)) + 4;
-    if (use_frame_decoder(h)) return h->ll_ws.ensure(cap * h->N * sizeof(double2));
+    if (use_frame_decoder(h)) return h->ll_ws.ensure(cap * (frame_le2_global(h->N) ? 2 : 1) * h->N * sizeof(double2));
     if (int rc = h->ll_ws.ensure(cap * ll_ws_elems(h->N) * sizeof(double2))) return rc;
     return h->ll_st.ensure(cap * ll_st_elems(h->N) * sizeof(float));
 }
@@ -1078,9 +1084,12 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
         if (int rc = order_on(h, st)) return rc;
         if (use_frame_decoder(h)) {
             if (int rc = frame_lds_attr(h->device)) return rc;
-            FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used};
-            hipLaunchKernelGGL(k_turbo_decode_frame, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true).total, st, a,
-                               (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ford);
+            const bool lg = frame_le2_global(h->N);
+            FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used,
+                     lg ? (double2 *)h->ll_ws.p + (size_t)B * h->N : nullptr};
+            hipLaunchKernelGGL(lg ? k_turbo_decode_frame<true> : k_turbo_decode_frame<false>, dim3((unsigned)B),
+                               dim3(FR_BLOCK), fr_lds(h->N, true, lg).total, st, a, (const int *)h->d_perm,
+                               (const int *)h->d_inv, (const int *)h->d_ford);
             HIPCHK(hipGetLastError());
             return mark_used(h, st);
         }

@@ -38,6 +38,8 @@
 // Same f32 / f64 operations as the reference everywhere; maxima are order-free
 // (fmaxf drops a NaN as the strict `>` does; only the sign of an exact zero can
 // differ, compared with IEEE ==).  tests/test_gpu_frame.py.
+#include <type_traits>
+
 namespace tdec {
 
 constexpr int FR_WAVES = 8;
@@ -67,7 +69,10 @@ __device__ __forceinline__ void lds_st(lds_b *p, float v) { *(lds_f1 *)p = v; }
 struct FrLds {
     int st_a, st_b, pmt, ev, sink, p1, le2, perm, inv, total;
 };
-__host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
+// le2_global (the decoder at N > 805, where the LDS plan is 8.5 KB over at N = 848):
+// decoder 2's extrinsic plane Le2 lives in the workgroup's own [N] double2 row of
+// global scratch (L2-resident) instead of LDS.
+__host__ __device__ constexpr FrLds fr_lds(int N, bool dec, bool le2_global = false) {
     FrLds L{};
     int o = 0;
     L.ev = o;   o += 2 * FR_NSEG_MAX * 64 + 64;   // 2 directions x 8 (16) segments; + the cross-wave rounds' control words
@@ -78,7 +83,7 @@ __host__ __device__ constexpr FrLds fr_lds(int N, bool dec) {
     L.p1 = L.le2 = L.perm = L.inv = o;
     if (dec) {
         L.p1 = o;    o += N * 16;
-        L.le2 = o;   o += N * 16;
+        L.le2 = o;   o += le2_global ? 0 : N * 16;
         L.perm = o;  o += N * 4;
         L.inv = o;   o += N * 4;
     }
@@ -617,13 +622,13 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
 // ord[0 .. n_used)); the SISO kernel's order is the identity.
 constexpr int FR_J = 2;                    // positions per thread: N <= FR_J * FR_BLOCK = 1024
 // get(raw, k): the f64 sums inA = f64(Lc_A) + La_A, inB (:135-136), the parities and Lc.
-struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[k]] (LDS)
+template <class P> struct FrIn1T {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[k]] (LDS or global)
     typedef float4 Raw;
-    const lds_b *le2;
+    P le2;   // lds_d2 * (LDS) or const double2 * (global scratch)
     const lds_int *inv;
     __device__ __forceinline__ void get(const Raw &x, int k, double &iA, double &iB, double &w, double &y, float &la,
                                         float &lb) const {
-        const d2v p = *(const lds_d2 *)(le2 + 16 * inv[k]);
+        const auto p = le2[inv[k]];
         iA = (double)x.x + p.x;
         iB = (double)x.y + p.y;
         w = x.z;
@@ -632,6 +637,7 @@ struct FrIn1 {   // decoder 1: planes X = {A, B, W1, Y1}, a-priori Le2[inv_perm[
         lb = x.y;
     }
 };
+typedef FrIn1T<const lds_d2 *> FrIn1;
 struct FrIn2 {   // decoder 2: planes Z = {W2, Y2}, P1[perm[k]] = f64(Lc) + Le1 (LDS; :507-516)
     typedef float2 Raw;
     const lds_b *p1;
@@ -676,11 +682,12 @@ struct FrOut1 {  // P1 = f64(Lc) + Le1 for decoder 2 (LDS), Le1 itself in the la
         if (le1) le1[k] = make_double2(a, b);
     }
 };
-struct FrOut2 {
-    lds_b *le2;
+template <class P> struct FrOut2T {
+    P le2;   // lds_d2 * or double2 *
     __device__ __forceinline__ int count(int N) const { return N; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
-        *(lds_d2 *)(le2 + 16 * k) = d2v{a, b};
+        if constexpr (std::is_same<P, double2 *>::value) le2[k] = make_double2(a, b);
+        else le2[k] = d2v{a, b};
     }
 };
 struct FrOutRow {
@@ -773,10 +780,13 @@ struct FrArgs {
     int32_t *bits;         // [B][2N]
     double *lfinal;        // [B][2N] or null
     int n_used;
+    double2 *le2;          // LG: [B][N] Le2 planes (global scratch)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) of one codeword per workgroup (grid = B).
 // ord: [N] the positions in perm's image (ascending), then the others.
+// LG: Le2 in global scratch (N > 805; see fr_lds).
+template <bool LG>
 __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
                                                                  const int *__restrict__ inv,
                                                                  const int *__restrict__ ord) {
@@ -784,13 +794,15 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
     lds_b *sm = (lds_b *)fr_sm;
     const int N = p.N, tid = threadIdx.x;
     const long cw = blockIdx.x;
-    const FrLds Lo = fr_lds(N, true);
+    const FrLds Lo = fr_lds(N, true, LG);
     const long tile = cw / WAVE;
     const int cwl = (int)(cw % WAVE);
     const float *base = p.planes + tile * tile_floats(N);
     const float4 *X = reinterpret_cast<const float4 *>(base);
     const float2 *Z = reinterpret_cast<const float2 *>(base + (long)N * WAVE * 4);
     lds_int *sperm = (lds_int *)(sm + Lo.perm), *sinv = (lds_int *)(sm + Lo.inv);
+    double2 *le2g = LG ? p.le2 + cw * N : nullptr;
+    lds_d2 *le2s = (lds_d2 *)(sm + Lo.le2);
     // this thread's positions and their planes, once for all 16 SISOs
     int pos[FR_J];
     float4 xr[FR_J];
@@ -806,15 +818,22 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
     for (int k = tid; k < N; k += FR_BLOCK) {
         sperm[k] = perm[k];
         sinv[k] = inv[k];
-        *(lds_d2 *)(sm + Lo.le2 + 16 * k) = d2v{0.0, 0.0};   // the first iteration's a-priori (:490-491)
+        if constexpr (LG) le2g[k] = make_double2(0.0, 0.0);   // the first iteration's a-priori (:490-491)
+        else le2s[k] = d2v{0.0, 0.0};
     }
-    __syncthreads();
+    __syncthreads();   // (a workgroup barrier orders the workgroup's global accesses too: one CU, one L1)
     double2 *le1 = p.le1 + cw * N;
     for (int it = 0; it < p.iters; ++it) {
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
-        fr_siso(FrIn1{sm + Lo.le2, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
-        fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2{sm + Lo.le2}, pos, zr, sm, Lo, N, sf);
+        if constexpr (LG) {
+            fr_siso(FrIn1T<const double2 *>{le2g, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm,
+                    Lo, N, sf);
+            fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2T<double2 *>{le2g}, pos, zr, sm, Lo, N, sf);
+        } else {
+            fr_siso(FrIn1{le2s, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
+            fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2T<lds_d2 *>{le2s}, pos, zr, sm, Lo, N, sf);
+        }
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
 #pragma unroll
@@ -822,10 +841,17 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
         const int k = pos[j];
         if (k < 0) continue;
         const float4 x = xr[j];
-        const d2v la = *(const lds_d2 *)(sm + Lo.le2 + 16 * sinv[k]);
+        double lax, lay;
+        if constexpr (LG) {
+            const double2 la = le2g[sinv[k]];
+            lax = la.x, lay = la.y;
+        } else {
+            const d2v la = le2s[sinv[k]];
+            lax = la.x, lay = la.y;
+        }
         const double2 le = le1[k];
-        const double fa = ((double)x.x + la.x) + le.x;
-        const double fb = ((double)x.y + la.y) + le.y;
+        const double fa = ((double)x.x + lax) + le.x;
+        const double fb = ((double)x.y + lay) + le.y;
         *reinterpret_cast<int2 *>(p.bits + cw * 2 * N + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
         if (p.lfinal) *reinterpret_cast<double2 *>(p.lfinal + cw * 2 * N + 2 * k) = make_double2(fa, fb);
     }

@@ -102,7 +102,7 @@ def test_frame_siso_adversarial(n, kind):
 
 
 @pytest.mark.parametrize("n,rate", [(48, "1/3"), (64, "3/4"), (212, "1/3"), (220, "2/3"), (424, "1/2"),
-                                    (752, "1/3"), (752, "1/2")])
+                                    (752, "1/3"), (752, "1/2"), (848, "1/3"), (848, "1/2")])
 @pytest.mark.parametrize("B,noise", [(1, 0.8), (2, 2.5), (65, 1.6)])
 def test_frame_decode_matches_oracle(n, rate, B, noise):
     rng = np.random.default_rng(n + B)
@@ -118,9 +118,11 @@ def test_frame_decode_matches_oracle(n, rate, B, noise):
 
 
 @pytest.mark.parametrize("kind", ["nan", "inf", "tiny"])
-def test_frame_decode_nonfinite_and_tiny(kind):
+@pytest.mark.parametrize("n", [212, 848])
+def test_frame_decode_nonfinite_and_tiny(kind, n):
+    """(N = 848: the frame decoder with Le2 in global scratch, tdec_frame.hip fr_lds)"""
     rng = np.random.default_rng(11)
-    c = M.DVBRCS2_Turbo(212, "1/3")
+    c = M.DVBRCS2_Turbo(n, "1/3")
     llr = (rng.standard_normal((3, c.n_coded)) * 2).astype(np.float32)
     if kind == "nan":
         llr[0, rng.integers(0, c.n_coded, 20)] = np.nan
@@ -143,6 +145,23 @@ def test_frame_decode_valid_perm_round_trip():
     info = rng.integers(0, 2, (4, c.k_info))
     llr = np.stack([(1 - 2.0 * c.encode(b)) * 20.0 for b in info]).astype(np.float32)
     assert np.array_equal(c.decode_batch(llr), info)
+
+
+def test_frame_decode_n848_batches_and_lfinal_every_row():
+    """N = 848 (a reference block size, dvb_rcs2_turbo.py:12-17): the frame decoder's
+    LDS plan is over 160 KiB there, so Le2 lives in global scratch; batches up to
+    the routing limit, every row against the oracle."""
+    rng = np.random.default_rng(848)
+    c = M.DVBRCS2_Turbo(848, "1/3")
+    B = 600
+    base = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in rng.integers(0, 2, (16, c.k_info))])
+    llr = (base[rng.integers(0, 16, B)] + rng.standard_normal((B, c.n_coded)) * 1.4).astype(np.float32)
+    for rows in (slice(0, 1), slice(0, 64), slice(0, B)):
+        bits, lf = c.decode_batch(llr[rows], return_lfinal=True)
+        rb, rl = O.decode_batch(llr[rows], c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
+                                c.inv_perm, TAB, want_lfinal=True, nthreads=16)
+        assert np.array_equal(bits, rb)
+        np.testing.assert_array_equal(lf, rl)
 
 
 def test_frame_decode_at_the_routing_threshold():

@@ -362,6 +362,7 @@ struct tdec_ctx {
     PinBuf pin;                        // page-locked staging of the small host-pointer calls
     PinBuf pin_siso;                   // the caller-filled SISO staging (tdec_siso_staging), never regrown behind its views
     int siso_rows = 0;                 //   rows it holds
+    unsigned siso_seq = 0;             //   the last call's sequence number in its completion flags (after the 8 slots)
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
@@ -1327,10 +1328,11 @@ int tdec_demap_stats(unsigned long long *out) {
 // the page-locked staging's device view for the zero-copy frame kernel).
 template <typename T>
 static int siso_launch(tdec_t *h, int n, const T *A, const T *B, const T *W, const T *Y, const double *la,
-                       const double *lb, double sf, double *ea, double *eb, bool fr, bool spl, hipStream_t s) {
+                       const double *lb, double sf, double *ea, double *eb, bool fr, bool spl, hipStream_t s,
+                       unsigned *done = nullptr) {
     constexpr bool F64 = sizeof(T) == 8;
     if (fr) {
-        FrSisoArgs fa{n, h->N, A, B, W, Y, la, lb, sf, ea, eb};
+        FrSisoArgs fa{n, h->N, A, B, W, Y, la, lb, sf, ea, eb, done, h->siso_seq};
         hipLaunchKernelGGL(k_siso_frame<T>, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
         HIPCHK(hipGetLastError());
         return 0;
@@ -1462,6 +1464,13 @@ static int siso_batch_impl(tdec_t *h, int B, const T *LcA, const T *LcB, const T
 // float32 channel-LLR row uses the first half of its slot.
 static size_t siso_slot(const tdec_t *h, int rows) { return ((size_t)rows * h->N * 8 + 255) / 256 * 256; }
 
+// TDEC_SPIN (read per call; default on): a zero-copy staged call waits for the frame
+// SISO's completion counter in the page-locked buffer instead of the stream.
+static bool spin_wait() {
+    const char *e = getenv("TDEC_SPIN");
+    return !(e && e[0] == '0');
+}
+
 template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
     constexpr bool F64 = sizeof(T) == 8;
     if (!h || B < 1 || B > h->siso_rows || !h->pin_siso.p) return fail(TDEC_EINVAL, "bad staged siso call (tdec_siso_staging first)");
@@ -1472,20 +1481,44 @@ template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
     siso_route(h, F64, fr, spl);
     int rc = fr ? frame_lds_attr(h->device) : ensure_ws(h, n_tiles_of(B));
     const size_t sl = siso_slot(h, h->siso_rows);
-    if (!rc && !(fr && zero_copy(B) && h->pin_siso.dev)) rc = h->h_misc.ensure(8 * sl);
+    const bool zc = fr && zero_copy(B) && h->pin_siso.dev;
+    if (!rc && !zc) rc = h->h_misc.ensure(8 * sl);
     if (rc) return rc;
     hipStream_t s = h->stream;
     char *dp;
-    if (fr && zero_copy(B) && h->pin_siso.dev) {
+    if (zc) {
         dp = (char *)h->pin_siso.dev;   // the kernel reads and writes the page-locked slots
     } else {
         dp = (char *)h->h_misc.p;
         HIPCHK(hipMemcpyAsync(dp, h->pin_siso.p, 6 * sl, hipMemcpyHostToDevice, s));
     }
+    volatile unsigned *flags = (volatile unsigned *)((char *)h->pin_siso.p + 8 * sl);
+    const bool spin = zc && spin_wait();
+    if (spin && ++h->siso_seq == 0) h->siso_seq = 1;   // flags start at 0: never a valid sequence number
     if ((rc = siso_launch<T>(h, B, (const T *)dp, (const T *)(dp + sl), (const T *)(dp + 2 * sl), (const T *)(dp + 3 * sl),
                              (const double *)(dp + 4 * sl), (const double *)(dp + 5 * sl), sf, (double *)(dp + 6 * sl),
-                             (double *)(dp + 7 * sl), fr, spl, s)))
+                             (double *)(dp + 7 * sl), fr, spl, s, spin ? (unsigned *)(dp + 8 * sl) : nullptr)))
         return rc;
+    if (spin) {
+        // The rows' outputs are in the page-locked slots once every row's flag holds
+        // this call's sequence number (a row sets it after fencing its stores).  The
+        // kernel may still be retiring when this returns; later work on the handle's
+        // stream is ordered behind it and nothing it touches afterwards is the
+        // caller's.  A kernel that never sets them (a fault) is caught by the stream
+        // wait after ~2^26 polls.
+        long polls = 0;
+        for (int r = 0; r < B; ++r)
+            while (flags[r] != h->siso_seq) {
+                if (++polls > (1L << 26)) {
+                    HIPCHK(hipStreamSynchronize(s));
+                    if (flags[r] != h->siso_seq) return fail(TDEC_EHIP, "frame SISO finished without flagging its rows");
+                    break;
+                }
+            }
+        drain.disarm();
+        mark_idle(h);
+        return 0;
+    }
     if (dp == (char *)h->h_misc.p)
         HIPCHK(hipMemcpyAsync((char *)h->pin_siso.p + 6 * sl, dp + 6 * sl, 2 * sl, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -1503,8 +1536,10 @@ int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes) {
         quiesce(h);
         h->pin_siso.release();   // the caller's views of the old buffer die with this call
         h->siso_rows = 0;
-        if (int rc = h->pin_siso.ensure(8 * siso_slot(h, rows))) return rc;
+        // + the per-row completion flags
+        if (int rc = h->pin_siso.ensure(8 * siso_slot(h, rows) + ((size_t)rows * 4 + 255) / 256 * 256)) return rc;
         h->siso_rows = rows;
+        std::memset((char *)h->pin_siso.p + 8 * siso_slot(h, rows), 0, (size_t)rows * 4);
     }
     *buf = h->pin_siso.p;
     *slot_bytes = siso_slot(h, h->siso_rows);

@@ -54,6 +54,24 @@ constexpr int FR_BLOCK = FR_WAVES * WAVE;
 #define TDEC_FR_WPD 2
 #endif
 constexpr int FR_NSEG_MAX = TDEC_FR_WPD == 4 ? 16 : 8;   // segments per direction at most
+// TDEC_FR_LMIN: the shortest segment (steps, a multiple of 4).  A segment shorter
+// than the recursions' typical merge depth (~40 steps) rarely merges in its first
+// re-run, so the rounds hand end vectors down a chain of segments: at N = 48 the
+// even split (8-step segments) made every SISO ~17 us of rounds and barriers where
+// one 48-step segment is two serial passes.  Measured (profiles/r05c/, host-pointer
+// calls, medians of two passes; segments of at least 0 / 32 / 48 / 64 / 96 steps):
+// decode() per frame N = 48: 0.291 / 0.183 / 0.148 / 0.147 / 0.148 ms; N = 212: 0.235 /
+// 0.223 / 0.207 / 0.217 / 0.239 ms; N = 752 unchanged (96-step segments either way);
+// bcjr_max_log_map N = 48: 0.041 / 0.033 / 0.029 / 0.029 / 0.029 ms.
+#ifndef TDEC_FR_LMIN
+#define TDEC_FR_LMIN 48
+#endif
+// segment length of a direction split over P segments: N / P rounded up to whole
+// 4-step blocks, at least TDEC_FR_LMIN
+__host__ __device__ constexpr int fr_seg_len(int N, int P) {
+    const int L = (N + 4 * P - 1) / (4 * P) * 4;
+    return L > TDEC_FR_LMIN ? L : TDEC_FR_LMIN;
+}
 typedef __attribute__((address_space(3))) char lds_b;   // byte-addressed LDS
 
 __device__ __forceinline__ float lds_ld(const lds_b *p) { return *(const lds_f1 *)p; }
@@ -404,7 +422,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     const int l = lane & 15, g = lane >> 4;
     const FrLane<DIR> L = fr_lane<DIR>(l);
     const int N = R.N;
-    const int Ls = (N + 15) / 16 * 4;       // segment length (a multiple of 4)
+    const int Ls = fr_seg_len(N, 4);        // segment length (a multiple of 4)
     const int nseg = (N + Ls - 1) / Ls;     // 1..4
     const int len = max(0, min(Ls, N - g * Ls)), u0 = len ? g * Ls : 0;   // empty segments never run
     const unsigned long long all = nseg == 4 ? ~0ull : (1ull << (16 * nseg)) - 1;
@@ -480,7 +498,7 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
         (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * FR_NSEG_MAX * 64);
     constexpr int WPDX = TDEC_FR_WPD > 1 ? TDEC_FR_WPD : 2;   // waves per direction
     static_assert(WPDX == 2 || WPDX == 4, "TDEC_FR_WPD: 1, 2 or 4");
-    const int Ls = (N + 16 * WPDX - 1) / (16 * WPDX) * 4;   // segment length (a multiple of 4)
+    const int Ls = fr_seg_len(N, 4 * WPDX);   // segment length (a multiple of 4)
     const int nseg = (N + Ls - 1) / Ls;     // 1..4 * WPDX
     const unsigned all = (1u << nseg) - 1;
     const bool rw = wave < 2 * WPDX;
@@ -864,6 +882,8 @@ struct FrSisoArgs {
     const double *LaA, *LaB;
     double sf;
     double *LeA, *LeB;
+    unsigned *done;   // nullable: host-mapped per-row completion flags, set to seq after the row's outputs
+    unsigned seq;
 };
 template <typename T> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
@@ -880,6 +900,13 @@ template <typename T> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(F
         raw[j] = in.fetch(i < p.N ? i : 0);
     }
     fr_siso(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
+    if (p.done) {
+        // every thread's extrinsic stores are system-visible before the row's flag:
+        // the host polls the flags instead of waiting for the kernel's end
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(p.done + blockIdx.x, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 }  // namespace tdec

@@ -104,13 +104,13 @@ def lane_step(v, pm_row, ph, idx):
     return (n - n[0]).astype(np.float32)
 
 
-def frame_recursion(pm, beta, P=4):
+def frame_recursion(pm, beta, P=4, lmin=0):
     """The kernel's engine: stored vectors [N][16] in step order (natural state
     order), after both passes, plus round statistics.  P segments per direction
     (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2; 16: four waves)."""
     N = pm.shape[0]
     lbl, idx = lane_consts(beta)
-    Ls = (N + 4 * P - 1) // (4 * P) * 4
+    Ls = max((N + 4 * P - 1) // (4 * P) * 4, lmin)      # tdec_frame.hip fr_seg_len (TDEC_FR_LMIN)
     nseg = (N + Ls - 1) // Ls
     seg = [(g * Ls, max(0, min(Ls, N - g * Ls))) for g in range(P)]
     st = np.full((N, 16), np.nan, np.float32)
@@ -209,10 +209,11 @@ def test_lane_step_equals_serial_step(beta):
 @pytest.mark.parametrize("N", [1, 2, 3, 5, 8, 13, 16, 17, 33, 48, 101, 212])
 @pytest.mark.parametrize("scale", [3.0, 1e-3])
 @pytest.mark.parametrize("P", [4, 8, 16])
-def test_segment_rounds_equal_two_pass(beta, N, scale, P):
+@pytest.mark.parametrize("lmin", [0, 48])
+def test_segment_rounds_equal_two_pass(beta, N, scale, P, lmin):
     rng = np.random.default_rng(N * 3 + int(beta))
     pm = _pm(rng, N, scale)
-    st, _ = frame_recursion(pm, beta, P)
+    st, _ = frame_recursion(pm, beta, P, lmin)
     np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
 
 
@@ -242,7 +243,7 @@ def test_segment_rounds_random_sweep_covers_every_path():
         if trial % 7 == 0:
             pm[rng.integers(0, N)] = np.nan
         beta = bool(trial % 2)
-        st, stats = frame_recursion(pm, beta, (4, 8, 16, 8)[trial % 4])
+        st, stats = frame_recursion(pm, beta, (4, 8, 16, 8)[trial % 4], (0, 0, 48, 32, 64)[trial % 5])
         np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
         seen.add((stats["spec"], stats["broken"]))
     assert {(True, False), (False, False), (False, True)} <= seen, seen

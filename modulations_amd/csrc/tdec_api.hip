@@ -967,12 +967,20 @@ static bool use_frame_decoder(const tdec_t *h) {
     const char *e = getenv("TDEC_FRAME");   // read per call: tests switch decoders in-process
     return !(e && e[0] == '0') && frame_fits(h->N, true);
 }
+// log-MAP batches the frame decoder takes (TDEC_LOWLAT_MAX overrides it too).  Measured
+// (profiles/r05/logmap_frame/, N = 752 r = 1/2, host-pointer calls): frame decoder
+// 1.08 / 1.32 / 5.30 / 20.4 / 43.1 ms at B = 1 / 64 / 1 024 / 4 096 / 8 192, the
+// throughput kernel 27.9 / 28.0 / 28.7 / 30.0 / 34.4 ms: the crossover is near 6 000.
+constexpr int LM_FRAME_MAX = 6144;
 static int lowlat_max(const tdec_t *h) {
     static const int v = [] {
         const char *e = getenv("TDEC_LOWLAT_MAX");
         return e ? std::max(0, atoi(e)) : -1;
     }();
-    if (h->algo != TDEC_ALGO_MAXLOG) return 0;
+    if (h->algo != TDEC_ALGO_MAXLOG) {   // log-MAP: the frame decoder only (the state-per-lane one is max-log)
+        if (!use_frame_decoder(h)) return 0;
+        return v >= 0 ? v : LM_FRAME_MAX;
+    }
     if (v >= 0) return v;
     // 8 192 was measured for the frame decoder only; the state-per-lane decoder's
     // own crossover is 4 096 (26.1 vs 20.2 ms at 8 192, profiles/r03llmax/)
@@ -980,7 +988,8 @@ static int lowlat_max(const tdec_t *h) {
 }
 // One predicate for "the small-batch decoders can run on this handle" (reserve and decode).
 static bool lowlat_usable(const tdec_t *h) {
-    return lowlat_max(h) > 0 && (use_frame_decoder(h) || ll_lds_bytes(h->N) <= 64 * 1024);
+    return lowlat_max(h) > 0 &&
+           (use_frame_decoder(h) || (h->algo == TDEC_ALGO_MAXLOG && ll_lds_bytes(h->N) <= 64 * 1024));
 }
 // Codewords the small-batch workspace holds for the decoder that would run (batches
 // up to that minus 4): the frame decoder keeps only Le1 (N double2 per row) outside
@@ -1002,8 +1011,10 @@ static int frame_lds_attr(int device) {
     if (device < 0 || device >= 256) return fail(TDEC_EINVAL, "device ordinal out of range");
     std::lock_guard<std::mutex> lk(mu);
     if (done[device]) return 0;
-    const void *fns[] = {(const void *)k_turbo_decode_frame<false>, (const void *)k_turbo_decode_frame<true>,
-                         (const void *)k_siso_frame<float>, (const void *)k_siso_frame<double>};
+    const void *fns[] = {(const void *)k_turbo_decode_frame<false, 0>, (const void *)k_turbo_decode_frame<true, 0>,
+                         (const void *)k_turbo_decode_frame<false, 1>, (const void *)k_turbo_decode_frame<true, 1>,
+                         (const void *)k_siso_frame<float, 0>, (const void *)k_siso_frame<double, 0>,
+                         (const void *)k_siso_frame<float, 1>, (const void *)k_siso_frame<double, 1>};
     for (const void *f : fns) {
         const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
         if (r != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(r));
@@ -1088,9 +1099,10 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
             const bool lg = frame_le2_global(h->N);
             FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used,
                      lg ? (double2 *)h->ll_ws.p + (size_t)B * h->N : nullptr};
-            hipLaunchKernelGGL(lg ? k_turbo_decode_frame<true> : k_turbo_decode_frame<false>, dim3((unsigned)B),
-                               dim3(FR_BLOCK), fr_lds(h->N, true, lg).total, st, a, (const int *)h->d_perm,
-                               (const int *)h->d_inv, (const int *)h->d_ford);
+            const auto kern = h->algo ? (lg ? k_turbo_decode_frame<true, 1> : k_turbo_decode_frame<false, 1>)
+                                      : (lg ? k_turbo_decode_frame<true, 0> : k_turbo_decode_frame<false, 0>);
+            hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true, lg).total, st, a,
+                               (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ford);
             HIPCHK(hipGetLastError());
             return mark_used(h, st);
         }
@@ -1333,7 +1345,8 @@ static int siso_launch(tdec_t *h, int n, const T *A, const T *B, const T *W, con
     constexpr bool F64 = sizeof(T) == 8;
     if (fr) {
         FrSisoArgs fa{n, h->N, A, B, W, Y, la, lb, sf, ea, eb, done, h->siso_seq};
-        hipLaunchKernelGGL(k_siso_frame<T>, dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
+        hipLaunchKernelGGL((h->algo ? k_siso_frame<T, 1> : k_siso_frame<T, 0>), dim3((unsigned)n), dim3(FR_BLOCK),
+                           fr_lds(h->N, false).total, s, fa);
         HIPCHK(hipGetLastError());
         return 0;
     }
@@ -1366,11 +1379,13 @@ static int siso_launch(tdec_t *h, int n, const T *A, const T *B, const T *W, con
 // Which SISO kernel serves a handle: max-log rows go to the frame SISO (one row per
 // workgroup, tdec_frame.hip; no workspace) unless TDEC_SISO_FRAME=0 (A/B) or its LDS
 // does not fit; TDEC_SISO_SPL=1 selects the state-per-lane prototype (float32 only).
-static void siso_route(const tdec_t *h, bool f64, bool &fr, bool &spl) {
+// log-MAP rows take the frame SISO up to LM_FRAME_MAX rows per call (the row kernel's
+// one lane per row is a serial chain of max* per codeword).
+static void siso_route(const tdec_t *h, bool f64, int B, bool &fr, bool &spl) {
     const char *se = getenv("TDEC_SISO_SPL");
     spl = !f64 && se && se[0] == '1' && h->algo == TDEC_ALGO_MAXLOG;
     const char *sfe = getenv("TDEC_SISO_FRAME");
-    fr = !spl && h->algo == TDEC_ALGO_MAXLOG && !(sfe && sfe[0] == '0') && frame_fits(h->N, false);
+    fr = !spl && (h->algo == TDEC_ALGO_MAXLOG || B <= LM_FRAME_MAX) && !(sfe && sfe[0] == '0') && frame_fits(h->N, false);
 }
 
 // tdec_siso_batch / tdec_siso_batch_f64: T = the channel LLRs' dtype.
@@ -1390,7 +1405,7 @@ static int siso_batch_impl(tdec_t *h, int B, const T *LcA, const T *LcB, const T
     const int C = (int)std::min<long>(B, chunk), waves = n_tiles_of(C);
     const size_t N = h->N, cf = (size_t)C * N * sizeof(T), cd = (size_t)C * N * sizeof(double);
     bool fr, spl;
-    siso_route(h, F64, fr, spl);
+    siso_route(h, F64, B, fr, spl);
     int rc = fr ? frame_lds_attr(h->device) : ensure_ws(h, waves);
     if (!rc) rc = h->h_misc.ensure(4 * cf + 4 * cd);
     if (rc) return rc;
@@ -1478,7 +1493,7 @@ template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
     quiesce(h);
     DrainOnExit drain{h->stream, nullptr};
     bool fr, spl;
-    siso_route(h, F64, fr, spl);
+    siso_route(h, F64, B, fr, spl);
     int rc = fr ? frame_lds_attr(h->device) : ensure_ws(h, n_tiles_of(B));
     const size_t sl = siso_slot(h, h->siso_rows);
     const bool zc = fr && zero_copy(B) && h->pin_siso.dev;

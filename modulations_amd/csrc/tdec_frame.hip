@@ -235,6 +235,23 @@ template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, fl
     return n - __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));   // row_newbcast:0
 }
 
+// log-MAP (ALGO 1): the same step with max* (jac, tdec_kernels.hip) over the lane's
+// own pair value and its partner's in place of max3 with -1e9 (alpha_step /
+// beta_step's jac(x0, y0) over a state's two predecessor / successor classes: jac
+// is symmetric, so which of the two the lane holds does not matter), then the
+// same state-0 normalisation.
+template <int PH> __device__ __forceinline__ float fr_step_lm(float v, float ps, float po) {
+    const float y = fr_partner_add<PH>(v, po);
+    const float n = jac(v + ps, y);
+    float r;
+    asm("s_nop 1\n\tv_subrev_f32_dpp %0, %1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(n));
+    return r;
+}
+template <int ALGO, int PH> __device__ __forceinline__ float fr_step_a(float v, const float (&c)[4]) {
+    if constexpr (ALGO == 1) return fr_step_lm<PH>(v, c[0], c[1]);
+    else return fr_step<PH>(v, c[0], c[1], c[2], c[3]);
+}
+
 // TDEC_FR_ASMBLK: a fast block (4 steps, each entering vector stored) as one asm
 // sequence -- the same instructions as fr_step / lds_st (own add, DPP partner add,
 // v_max3 with -1e9, DPP normalisation by lane 0), so the same bits, with each store
@@ -326,7 +343,7 @@ __device__ unsigned long long g_fr_stats[8];   // blocks run: phase A, fix-up, p
 // block start where its vector equals the stored one (merged).  Returns the
 // lanes of the groups that reached their segment's end (their end vector, the
 // one entering step u0 + len, is in ev[g]).
-template <int DIR, bool CMP>
+template <int DIR, bool CMP, int ALGO = 0>
 __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrLane<DIR> &L, int g, int lane, int u0,
                                                        int len, unsigned long long run, float v, int stat) {
     const int N = R.N;
@@ -378,18 +395,18 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         lds_b *const srw = R.st + srow(U);
         if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
             lds_b *const sr = rl ? srw : sink_s;
-            if constexpr (TDEC_FR_ASMBLK && TDEC_FR_ASM && !TDEC_FR_N0 && !TDEC_FR_EXP) {
+            if constexpr (ALGO == 0 && TDEC_FR_ASMBLK && TDEC_FR_ASM && !TDEC_FR_N0 && !TDEC_FR_EXP) {
                 fr_block_asm(v, c, (unsigned)(uintptr_t)(sr + L.soff[0]), (unsigned)(uintptr_t)(sr + L.soff[1]),
                              (unsigned)(uintptr_t)(sr + L.soff[2]), (unsigned)(uintptr_t)(sr + L.soff[3]));
             } else {
                 if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[0], v);
-                v = fr_step<0>(v, c[0][0], c[0][1], c[0][2], c[0][3]);
+                v = fr_step_a<ALGO, 0>(v, c[0]);
                 if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[1], v);
-                v = fr_step<1>(v, c[1][0], c[1][1], c[1][2], c[1][3]);
+                v = fr_step_a<ALGO, 1>(v, c[1]);
                 if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[2], v);
-                v = fr_step<2>(v, c[2][0], c[2][1], c[2][2], c[2][3]);
+                v = fr_step_a<ALGO, 2>(v, c[2]);
                 if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[3], v);
-                v = fr_step<3>(v, c[3][0], c[3][1], c[3][2], c[3][3]);
+                v = fr_step_a<ALGO, 3>(v, c[3]);
             }
         } else {   // some group ends in this block: per-step bounds, end vector captured
             lds_b *const evg = R.ev + g * 64;
@@ -397,7 +414,7 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
     {                                                                          \
         const int uu = u + PH;                                                 \
         if (rl && uu < len) lds_st(srw + L.soff[PH], v);                       \
-        const float vn = fr_step<PH>(v, c[PH][0], c[PH][1], c[PH][2], c[PH][3]);   \
+        const float vn = fr_step_a<ALGO, PH>(v, c[PH]);                             \
         if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(PH + 1) & 3], vn);    \
         v = vn;                                                                \
     }
@@ -418,7 +435,7 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
 
 // Both passes of one direction (alpha: :162-197, beta: :199-230) by one wave.
 // On exit row k of R.st holds alpha2[k] (k < N) / beta2[k] (k >= 1).
-template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
+template <int DIR, int ALGO = 0> __device__ void fr_recursion(const FrRec &R, int lane) {
     const int l = lane & 15, g = lane >> 4;
     const FrLane<DIR> L = fr_lane<DIR>(l);
     const int N = R.N;
@@ -428,7 +445,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
     const unsigned long long all = nseg == 4 ? ~0ull : (1ull << (16 * nseg)) - 1;
     const lds_b *src = R.ev + (g == 0 ? nseg - 1 : g - 1) * 64 + 4 * L.lbl[0];   // the start of a re-run
     // pass 1, phase A: every segment from zero (segment 0: the reference's start)
-    unsigned long long reached = fr_round<DIR, false>(R, L, g, lane, u0, len, all, 0.0f, 0);
+    unsigned long long reached = fr_round<DIR, false, ALGO>(R, L, g, lane, u0, len, all, 0.0f, 0);
     unsigned long long dirty = (reached << 16) & all;
     // The first re-run round also starts the reference's second pass SPECULATIVELY:
     // group 0 (idle in the re-runs) runs from the last segment's phase-A end
@@ -443,7 +460,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 #if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty | G0, lds_ld(src), 1);
+        reached = fr_round<DIR, true, ALGO>(R, L, g, lane, u0, len, dirty | G0, lds_ld(src), 1);
         const unsigned long long r1 = reached & ~G0;
         spec = !(r1 & GL);              // the last segment's end vector did not change
         dirty = (r1 << 16) & all;
@@ -461,7 +478,7 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 #if TDEC_FR_STATS == 1
             if (lane == 0) atomicAdd(&g_fr_stats[3], 1ull);
 #endif
-            reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
+            reached = fr_round<DIR, true, ALGO>(R, L, g, lane, u0, len, dirty, lds_ld(src), 1);
             dirty = (reached << 16) & all;
         }
     }
@@ -471,14 +488,14 @@ template <int DIR> __device__ void fr_recursion(const FrRec &R, int lane) {
 #if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, G0, lds_ld(src), 2);
+        reached = fr_round<DIR, true, ALGO>(R, L, g, lane, u0, len, G0, lds_ld(src), 2);
         dirty = ((reached & G0) || broken) ? (G0 << 16) & all : 0ull;
     }
     while (dirty) {
 #if TDEC_FR_STATS == 1
         if (lane == 0) atomicAdd(&g_fr_stats[4], 1ull);
 #endif
-        reached = fr_round<DIR, true>(R, L, g, lane, u0, len, dirty, lds_ld(src), 2);
+        reached = fr_round<DIR, true, ALGO>(R, L, g, lane, u0, len, dirty, lds_ld(src), 2);
         dirty = (reached << 16) & all;
     }
 }
@@ -493,7 +510,7 @@ struct FrCtl {
     unsigned dirty[2], reached[2], state[2], broken[2], cmp[2];
 };
 enum { FR_A = 0, FR_FIX1 = 1, FR_FIXN = 2, FR_P2S = 3, FR_P2 = 4 };
-__device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int lane) {
+template <int ALGO = 0> __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int lane) {
     volatile __attribute__((address_space(3))) FrCtl *ctl =
         (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * FR_NSEG_MAX * 64);
     constexpr int WPDX = TDEC_FR_WPD > 1 ? TDEC_FR_WPD : 2;   // waves per direction
@@ -543,10 +560,10 @@ __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int 
 #endif
             unsigned long long r;
             const int stat = cmp ? (ctl->state[dir] == FR_P2 || ctl->state[dir] == FR_P2S ? 2 : 1) : 0;
-            if (dir == 0) r = cmp ? fr_round<0, true>(Ra, La, G, lane, u0, len, run, v, stat)
-                                  : fr_round<0, false>(Ra, La, G, lane, u0, len, run, v, stat);
-            else r = cmp ? fr_round<1, true>(Rb, Lb, G, lane, u0, len, run, v, stat)
-                         : fr_round<1, false>(Rb, Lb, G, lane, u0, len, run, v, stat);
+            if (dir == 0) r = cmp ? fr_round<0, true, ALGO>(Ra, La, G, lane, u0, len, run, v, stat)
+                                  : fr_round<0, false, ALGO>(Ra, La, G, lane, u0, len, run, v, stat);
+            else r = cmp ? fr_round<1, true, ALGO>(Rb, Lb, G, lane, u0, len, run, v, stat)
+                         : fr_round<1, false, ALGO>(Rb, Lb, G, lane, u0, len, run, v, stat);
             unsigned bits = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -719,7 +736,7 @@ struct FrOutRow {
 
 // One SISO (:116-281) of the workgroup's codeword.  pos[j]: this thread's positions
 // (-1: none), raw[j] their channel values.  Ends with a barrier.
-template <class In, class Out>
+template <int ALGO, class In, class Out>
 __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], const typename In::Raw (&raw)[FR_J],
                         lds_b *sm, const FrLds &Lo, int N, double sf) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -736,8 +753,9 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
         float la, lb;
         in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8], pm[2][4];
-        gamma_from_sums(iA, iB, w, y, g);
-        pair_max(g, pm);
+        gamma_from_sums<ALGO>(iA, iB, w, y, g);
+        if constexpr (ALGO == 1) pair_jac(g, pm);   // log-MAP pair values v(wy) + max*(U_c, -U_c)
+        else pair_max(g, pm);
         lds_f4 *d = (lds_f4 *)(pmt + 32 * k);
         d[0] = f4v{pm[0][0], pm[0][1], pm[0][2], pm[0][3]};
         d[1] = f4v{pm[1][0], pm[1][1], pm[1][2], pm[1][3]};
@@ -748,10 +766,10 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
 #endif
     // R: alpha on wave 0, beta on wave 1 (TDEC_FR_WPD 2: alpha on waves 0-1, beta on 2-3)
     if constexpr (TDEC_FR_WPD == 1) {
-        if (wave == 0) fr_recursion<0>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
-        else if (wave == 1) fr_recursion<1>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N}, lane);
+        if (wave == 0) fr_recursion<0, ALGO>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
+        else if (wave == 1) fr_recursion<1, ALGO>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N}, lane);
     } else {
-        fr_recursion_x(sm, Lo, N, wave, lane);
+        fr_recursion_x<ALGO>(sm, Lo, N, wave, lane);
     }
     __syncthreads();
 #if TDEC_FR_STATS
@@ -767,7 +785,7 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
         float la, lb;
         in.get(raw[j], k, iA, iB, w, y, la, lb);
         float g[8];
-        gamma_from_sums(iA, iB, w, y, g);
+        gamma_from_sums<ALGO>(iA, iB, w, y, g);
         float a[NS], b[NS];
         const lds_f4 *ra = (const lds_f4 *)(sm + Lo.st_a + 64 * k), *rb = (const lds_f4 *)(sm + Lo.st_b + 64 * (k + 1));
 #pragma unroll
@@ -777,7 +795,7 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
             b[4 * q] = z.x, b[4 * q + 1] = z.y, b[4 * q + 2] = z.z, b[4 * q + 3] = z.w;
         }
         double leA, leB;
-        extrinsic<0>(a, g, b, iA, iB, sf, leA, leB);
+        extrinsic<ALGO>(a, g, b, iA, iB, sf, leA, leB);
         out.store(k, leA, leB, la, lb);
     }
     __syncthreads();
@@ -804,7 +822,7 @@ struct FrArgs {
 // DVBRCS2_Turbo.decode (:464-537) of one codeword per workgroup (grid = B).
 // ord: [N] the positions in perm's image (ascending), then the others.
 // LG: Le2 in global scratch (N > 805; see fr_lds).
-template <bool LG>
+template <bool LG, int ALGO = 0>
 __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
                                                                  const int *__restrict__ inv,
                                                                  const int *__restrict__ ord) {
@@ -845,12 +863,12 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
         if constexpr (LG) {
-            fr_siso(FrIn1T<const double2 *>{le2g, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm,
-                    Lo, N, sf);
-            fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2T<double2 *>{le2g}, pos, zr, sm, Lo, N, sf);
+            fr_siso<ALGO>(FrIn1T<const double2 *>{le2g, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos,
+                          xr, sm, Lo, N, sf);
+            fr_siso<ALGO>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<double2 *>{le2g}, pos, zr, sm, Lo, N, sf);
         } else {
-            fr_siso(FrIn1{le2s, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
-            fr_siso(FrIn2{sm + Lo.p1, sperm}, FrOut2T<lds_d2 *>{le2s}, pos, zr, sm, Lo, N, sf);
+            fr_siso<ALGO>(FrIn1{le2s, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
+            fr_siso<ALGO>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<lds_d2 *>{le2s}, pos, zr, sm, Lo, N, sf);
         }
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
@@ -885,7 +903,7 @@ struct FrSisoArgs {
     unsigned *done;   // nullable: host-mapped per-row completion flags, set to seq after the row's outputs
     unsigned seq;
 };
-template <typename T> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
+template <typename T, int ALGO = 0> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;
     const long row = (long)blockIdx.x * p.N;
@@ -899,7 +917,7 @@ template <typename T> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(F
         pos[j] = i < p.N ? i : -1;
         raw[j] = in.fetch(i < p.N ? i : 0);
     }
-    fr_siso(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
+    fr_siso<ALGO>(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
     if (p.done) {
         // every thread's extrinsic stores are system-visible before the row's flag:
         // the host polls the flags instead of waiting for the kernel's end

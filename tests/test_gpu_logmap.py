@@ -130,3 +130,81 @@ def test_logmap_gpu_siso_within_1e5_of_exact_log_map():
         big = max(np.max(np.abs(Lc[0, 0] + La[0, 0])), np.max(np.abs(Lc[1, 0] + La[1, 0])))
         tol = 1e-5 if i < 3 else 1e-5 + 2 * 2.0 ** -23 * big
         assert max(np.max(np.abs(A[0] - RA)), np.max(np.abs(B[0] - RB))) <= tol, (sc, lsc, n)
+
+
+# ---- the frame decoder / frame SISO in log-MAP (round 5): small batches ---------------
+# One codeword per workgroup (tdec_frame.hip, ALGO 1): the pair values v(wy) + max*(U_c,
+# -U_c) in the LDS table, the recursions' step with max* over the two predecessor
+# (successor) classes, segments that re-run until they merge, extrinsic<1>.  Batches up
+# to LM_FRAME_MAX codewords take it (decode() per frame was one lane of the throughput
+# kernel: ~28 ms at N = 752); compared with the oracle's log-MAP (algo 1, the device's
+# primitive tables) bit for bit, bits and L_final.
+@pytest.mark.parametrize("n,rate", [(48, "1/3"), (212, "1/3"), (752, "1/2"), (848, "1/3"), (220, "2/3")])
+@pytest.mark.parametrize("B,noise", [(1, 1.0), (3, 2.2), (65, 1.5)])
+def test_logmap_frame_decode_matches_oracle(n, rate, B, noise):
+    rng = np.random.default_rng(n * 3 + B)
+    c = M.DVBRCS2_Turbo(n, rate, algo="log-map")
+    info = rng.integers(0, 2, (B, c.k_info))
+    llr = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in info]).astype(np.float32)
+    llr += (rng.standard_normal(llr.shape) * noise).astype(np.float32)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    t, _ = O.trellis()
+    rb, rl = O.decode_batch(llr, c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
+                            c.inv_perm, t, algo=1, want_lfinal=True, nthreads=16)
+    assert np.array_equal(bits, rb)
+    np.testing.assert_array_equal(lf, rl)
+    if B == 1:
+        assert np.array_equal(c.decode(llr[0]), rb[0])     # decode() per frame, test.py:81
+
+
+@pytest.mark.parametrize("kind", ["nan", "inf", "tiny", "huge"])
+def test_logmap_frame_decode_edge_inputs(kind):
+    rng = np.random.default_rng(7)
+    c = M.DVBRCS2_Turbo(212, "1/3", algo="log-map")
+    llr = (rng.standard_normal((3, c.n_coded)) * 2).astype(np.float32)
+    if kind == "nan":
+        llr[0, rng.integers(0, c.n_coded, 20)] = np.nan
+        llr[2, :] = np.nan
+    elif kind == "inf":
+        llr[0, rng.integers(0, c.n_coded, 20)] = np.inf
+        llr[1, rng.integers(0, c.n_coded, 20)] = -np.inf
+    elif kind == "tiny":
+        llr *= np.float32(1e-4)
+    else:
+        llr *= np.float32(1e4)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    t, _ = O.trellis()
+    rb, rl = O.decode_batch(llr, c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
+                            c.inv_perm, t, algo=1, want_lfinal=True, nthreads=8)
+    assert np.array_equal(bits, rb)
+    np.testing.assert_array_equal(lf, rl)
+
+
+def test_logmap_frame_equals_throughput_decoder():
+    """4 096 codewords through the frame decoder, 4 097 (one more than its limit)
+    through the persistent throughput kernel: the same bits on the shared rows."""
+    rng = np.random.default_rng(4097)
+    c = M.DVBRCS2_Turbo(752, "1/2", algo="log-map")
+    base = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in rng.integers(0, 2, (32, c.k_info))])
+    llr = (base[rng.integers(0, 32, 4097)] + rng.standard_normal((4097, c.n_coded)) * 1.5).astype(np.float32)
+    b_frame, l_frame = c.decode_batch(llr[:4096], return_lfinal=True)
+    b_tp, l_tp = c.decode_batch(llr, return_lfinal=True)
+    assert np.array_equal(b_frame, b_tp[:4096])
+    np.testing.assert_array_equal(l_frame, l_tp[:4096])
+
+
+@pytest.mark.parametrize("n", [1, 5, 48, 212, 752, 848, 1000])
+@pytest.mark.parametrize("lc", ["f32", "f64"])
+def test_logmap_frame_siso_matches_oracle(n, lc):
+    rng = np.random.default_rng(n + 5)
+    t, _ = O.trellis()
+    B = 3
+    Lc = [rng.standard_normal((B, n)) * 3 for _ in range(4)]
+    if lc == "f32":
+        Lc = [x.astype(np.float32) for x in Lc]
+    La = [rng.standard_normal((B, n)) * 9 for _ in range(2)]
+    A, Bv = M.bcjr_max_log_map_batch(*Lc, *La, *t, n, 0.7, algo="log-map")
+    for r in range(B):
+        ra, rb = O.siso(*(x[r] for x in Lc), *(x[r] for x in La), t, 0.7, algo=1)
+        np.testing.assert_array_equal(A[r], ra)
+        np.testing.assert_array_equal(Bv[r], rb)

@@ -489,6 +489,26 @@ __device__ __forceinline__ double2 ld2(const lds_d2 *p) {
 __device__ __forceinline__ unsigned lds_addr(const lds_void *l) {
     return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
 }
+// TDEC_GLDS_SADDR: the staging DMAs address memory as a wave-uniform 64-bit base in
+// SGPRs plus a 32-bit per-lane byte offset (the instruction's saddr form) instead of
+// a 64-bit per-lane address: one VGPR per address instead of a pair (the paired
+// addresses of the backward passes' prologues were spilled).
+#ifndef TDEC_GLDS_SADDR
+#define TDEC_GLDS_SADDR 1
+#endif
+__device__ __forceinline__ const void *uni_ptr(const void *p) {
+    const unsigned long long u = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    return (const void *)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ void glds16s(const void *base, unsigned off, lds_void *l) {
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds_addr(l)), "v"(off), "s"(uni_ptr(base))
+                 : "memory");
+}
+__device__ __forceinline__ void glds4s(const void *base, unsigned off, lds_void *l) {
+    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2" ::"s"(lds_addr(l)), "v"(off), "s"(uni_ptr(base))
+                 : "memory");
+}
 __device__ __forceinline__ void glds16(const void *g, lds_void *l) {
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr(l)), "v"(g) : "memory");
 }
@@ -533,8 +553,13 @@ struct TileIn {
         make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
-        glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
-        glds16(&at(La, wsrow(la_idx[k], rs) + lane), st.l + j * WAVE);
+        if constexpr (TDEC_GLDS_SADDR) {
+            glds16s(X, (unsigned)(k * WAVE + lane) * 16u, st.v + j * WAVE);
+            glds16s(La, (wsrow(la_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
+        } else {
+            glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
+            glds16(&at(La, wsrow(la_idx[k], rs) + lane), st.l + j * WAVE);
+        }
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         Raw r;
@@ -571,9 +596,16 @@ struct TileInPre {
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         const float *z = reinterpret_cast<const float *>(&at(Z, k * WAVE + lane));
         lds_f1 *dst = reinterpret_cast<lds_f1 *>(st.v + j * WAVE);
-        glds4(z, dst);
-        glds4(z + 1, dst + WAVE);
-        glds16(&at(P, wsrow(p_idx[k], rs) + lane), st.l + j * WAVE);
+        if constexpr (TDEC_GLDS_SADDR) {
+            const unsigned zo = (unsigned)(k * WAVE + lane) * 8u;
+            glds4s(Z, zo, dst);
+            glds4s(Z, zo + 4u, dst + WAVE);
+            glds16s(P, (wsrow(p_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
+        } else {
+            glds4(z, dst);
+            glds4(z + 1, dst + WAVE);
+            glds16(&at(P, wsrow(p_idx[k], rs) + lane), st.l + j * WAVE);
+        }
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         const lds_f1 *zp = reinterpret_cast<const lds_f1 *>(st.v + j * WAVE);
@@ -1273,7 +1305,10 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 // registers across the top half.
 __device__ __forceinline__ void ck_stage(const float4 *ck, unsigned cs, unsigned base, int lane, lds_f4 *slot) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) glds16(&at(ck, (base + q) * cs + lane), slot + q * WAVE);
+    for (int q = 0; q < 4; ++q) {
+        if constexpr (TDEC_GLDS_SADDR) glds16s(ck, ((base + q) * cs + lane) * 16u, slot + q * WAVE);
+        else glds16(&at(ck, (base + q) * cs + lane), slot + q * WAVE);
+    }
 }
 __device__ __forceinline__ void ck_read(const lds_f4 *slot, int lane, float (&x)[NS]) {
 #pragma unroll
@@ -1484,6 +1519,9 @@ __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
 __device__ __forceinline__ void merge_mark(int, int, int) {}
 #endif
 
+#ifndef TDEC_LAUNDER_LANE
+#define TDEC_LAUNDER_LANE 1
+#endif
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
                       const LdsStage &lb, const LdsStage &lb1, const Prio &pr = Prio{}) {
@@ -1557,12 +1595,20 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
 #endif
     for (int pass = 0; pass < 2; ++pass) {
         if (TDEC_PRIO_FINE && pass == 1) phase_prio(false, pr, 3);
+        // TDEC_LAUNDER_LANE: the lane index goes through an empty asm here, so the
+        // per-lane addresses of this prologue are formed from it again (a shift and
+        // an add each) instead of hoisted out of the tile's loops and spilled: the
+        // spilled ones came back through scratch loads, each followed by a full
+        // vmcnt(0) wait ahead of the DMA that needed it.
+        In inp = in;
+        int lanep = lane;
+        if constexpr (TDEC_LAUNDER_LANE) asm volatile("" : "+v"(inp.lane), "+v"(lanep));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            raw[j] = in.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
-            in.stage(RAG ? min(top + j, N - 1) : top + j, lb, j);
+            raw[j] = inp.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
+            inp.stage(RAG ? min(top + j, N - 1) : top + j, lb, j);
         }
-        ck_stage(ck, cs, (top / CK) * 4, lane, lb.ck);
+        ck_stage(ck, cs, (top / CK) * 4, lanep, lb.ck);
         merged = false;
         mlane = mwave = MH_END;
         for (int k0 = top; k0 >= 0; k0 -= WS) {

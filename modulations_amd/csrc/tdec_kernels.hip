@@ -128,7 +128,15 @@ __device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two IEEE f32 ops per lane
 
+// TDEC_LM_FAST (timing experiment, DIFFERENT BITS from the oracle): the same max*
+// without the +8 that bounds the instruction's argument grid, max + log2(1 +
+// 2^-|a-b|) (one VALU operation fewer per max*, two per lse4) -- measures what the
+// bit-exact pinning of the hardware primitives costs.
+#ifndef TDEC_LM_FAST
+#define TDEC_LM_FAST 0
+#endif
 __device__ __forceinline__ float jac(float a, float b) {
+    if constexpr (TDEC_LM_FAST) return fmaxf(a, b) + hw_log2(1.0f + hw_exp2(-fabsf(a - b)));
     const float t = fabsf(a - b) + LM_C;
     const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
     return fmaxf(a, b) + hw_log2(w);
@@ -138,6 +146,10 @@ __device__ __forceinline__ float jac(float a, float b) {
 // order by fma, plus Mc - 8 (exact: the maximum rounded to Mc's grid, the shift
 // the terms were taken against).
 __device__ __forceinline__ float lse4(float x0, float x1, float x2, float x3) {
+    if constexpr (TDEC_LM_FAST) {
+        const float M = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3));
+        return M + hw_log2(((hw_exp2(x0 - M) + hw_exp2(x1 - M)) + hw_exp2(x2 - M)) + hw_exp2(x3 - M));
+    }
     const float Mc = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)) + LM_C;
     float S = hw_exp2(-(Mc - x0)) * LM_SCALE;   // = fma(e, 256, 0): exact
     S = fmaf(hw_exp2(-(Mc - x1)), LM_SCALE, S);

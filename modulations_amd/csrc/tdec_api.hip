@@ -367,6 +367,8 @@ struct tdec_ctx {
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
     DevBuf ll_ws, ll_st;               // small-batch decoders: extrinsic planes (frame: Le1 only), alpha / beta stores
+    DevBuf iq_le2, iq_ctl, iq_ring;    // the throughput decoders' item queue (TDEC_ITEMQ): per-tile Le2, control, rings
+    int iq_tiles = 0;                  //   tiles they are sized for
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // uploads of the chunked host-pointer path (created on first use)
     hipStream_t dstream = nullptr;     // its downloads (a second copy engine direction)
@@ -675,6 +677,9 @@ void tdec_destroy(tdec_t *h) {
     h->planes_w.release();
     h->ll_ws.release();
     h->ll_st.release();
+    h->iq_le2.release();
+    h->iq_ctl.release();
+    h->iq_ring.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->dstream) hipStreamDestroy(h->dstream);
@@ -1048,6 +1053,28 @@ static int ensure_decl(tdec_t *h, long n_tiles) {
     return 0;
 }
 
+// TDEC_ITEMQ (read per call; build default TDEC_ITEMQ_DEFAULT): the throughput
+// decoders take (tile, iteration) items from per-XCD queues instead of whole tiles
+// per wave (tdec_kernels.hip, DecodeArgs::le2t).
+#ifndef TDEC_ITEMQ_DEFAULT
+#define TDEC_ITEMQ_DEFAULT 0
+#endif
+static bool itemq_on() {
+    const char *e = getenv("TDEC_ITEMQ");
+    return e ? e[0] == '1' : TDEC_ITEMQ_DEFAULT != 0;
+}
+static long iq_cap_of(const tdec_t *h, int tiles) { return std::max(1L, (long)(h->iters - 1) * tiles); }
+// per-tile Le2 ([tiles][N][64] double2), the control block and the rings; the caller
+// has quiesced the handle
+static int ensure_itemq(tdec_t *h, int tiles) {
+    if (tiles <= h->iq_tiles) return 0;
+    if (int rc = h->iq_le2.ensure((size_t)tiles * h->N * WAVE * sizeof(double2))) return rc;
+    if (int rc = h->iq_ctl.ensure(32 * 9 * sizeof(int))) return rc;
+    if (int rc = h->iq_ring.ensure((size_t)8 * iq_cap_of(h, tiles) * sizeof(int))) return rc;
+    h->iq_tiles = tiles;
+    return 0;
+}
+
 int tdec_reserve(tdec_t *h, int max_batch) {
     if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
     if (max_batch == 0) return 0;
@@ -1065,9 +1092,11 @@ int tdec_reserve(tdec_t *h, int max_batch) {
     if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap ||
         n_tiles_of(max_batch) > h->decl_tiles)
         quiesce(h);   // regrowth frees
+    if (itemq_on() && n_tiles_of(max_batch) > h->iq_tiles) quiesce(h);
     int rc = ensure_ws(h, want_waves);
     if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
     if (!rc) rc = ensure_decl(h, n_tiles_of(max_batch));
+    if (!rc && itemq_on()) rc = ensure_itemq(h, n_tiles_of(max_batch));
     if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
     return rc;
 }
@@ -1120,6 +1149,15 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     if (h->d_simd_prog && hipMemsetAsync(h->d_simd_prog, 0, SIMD_PROG_BYTES, st) == hipSuccess) a.simd_prog = h->d_simd_prog;
+    if (itemq_on() && tiles <= h->iq_tiles) {   // reserved by tdec_reserve; otherwise whole tiles per wave
+        HIPCHK(hipMemsetAsync(h->iq_ctl.p, 0, 32 * 9 * sizeof(int), st));
+        HIPCHK(hipMemsetAsync(h->iq_ring.p, 0, (size_t)8 * iq_cap_of(h, tiles) * sizeof(int), st));
+        a.le2t = (double2 *)h->iq_le2.p;
+        a.iq_ctl = (int *)h->iq_ctl.p;
+        a.iq_ring = (int *)h->iq_ring.p;
+        a.iq_cap = (int)iq_cap_of(h, tiles);
+        a.tile_ctr = nullptr;
+    }
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(DEC_BLOCK), 0, st,

@@ -1740,6 +1740,20 @@ struct DecodeArgs {
     int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
     int ck_rows;             // checkpoint rows before the beta1 ring: ceil(N / ck_win_of(algo))
     int *simd_prog = nullptr;   // TDEC_PRIO 4: [8192 SIMDs][16 wave slots] progress, zeroed per launch
+    // Item queue (TDEC_ITEMQ; null: each wave decodes whole tiles): work items are
+    // (tile, iteration).  A tile's first iteration is claimed from the chip-wide
+    // counter iq_ctl[0]; each later one is pushed to the claiming wave's XCD and
+    // taken by any wave of that XCD, so waves that run faster (alone on their SIMD,
+    // or idle at the end) take over iterations of the tiles of slower ones.  Le2
+    // then lives per TILE (le2t, [n_tiles][N][64]), handed from wave to wave inside
+    // one XCD (its L2 is shared; the taker invalidates its CU's L1 first).
+    // iq_ctl (zeroed per launch): [0] fresh-tile counter, then per XCD x at
+    // 32 * (x + 1): [0] tiles claimed, [1] items pushed, [2] items taken, [3] waves waiting;
+    // iq_ring [8][iq_cap]: entries tile * iters + iteration + 1 (0 = not yet written).
+    double2 *le2t = nullptr;
+    int *iq_ctl = nullptr;
+    int *iq_ring = nullptr;
+    int iq_cap = 0;
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1790,6 +1804,79 @@ __device__ __forceinline__ void progress_prio(int it, int iters) {
     if constexpr (TDEC_PRIO == 1) set_prio(3 - (4 * it) / iters);
 }
 
+// ---- the (tile, iteration) item queue (DecodeArgs::le2t) -------------------------------
+__device__ __forceinline__ int iq_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int iq_add(int *p, int v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Push item (this wave's XCD): reserve a ring slot, then write the entry (agent-scope
+// stores: the taker polls it past its L1).  Lane 0 only.
+// TDEC_IQ_YIELD: when a wave of the XCD is waiting for work, the pusher sleeps about
+// that many microseconds before it looks for its next item, so the waiting wave
+// (its SIMD otherwise idle) takes the pushed iteration and the pusher's SIMD sheds
+// a wave; without it the pusher nearly always takes its own item back.
+#ifndef TDEC_IQ_YIELD
+#define TDEC_IQ_YIELD 4
+#endif
+__device__ __forceinline__ void iq_push(const DecodeArgs &p, unsigned xcc, int lane, int item) {
+    bool yield = false;
+    if (lane == 0) {
+        int *c = p.iq_ctl + 32 * (xcc + 1);
+        const int slot = iq_add(c + 1, 1);
+        __hip_atomic_store(p.iq_ring + (long)xcc * p.iq_cap + slot, item + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        yield = TDEC_IQ_YIELD > 0 && iq_ld(c + 3) > 0;
+    }
+    if (__builtin_amdgcn_readfirstlane(yield ? 1 : 0))
+        for (int i = 0; i < 4 * TDEC_IQ_YIELD; ++i) __builtin_amdgcn_s_sleep(127);   // ~8k cycles: ~4 per us
+}
+// The wave's next item: a pushed iteration of this XCD's tiles first, else a fresh
+// tile (its iteration 0; the tile then belongs to this XCD), else -1 once every item
+// of this XCD has been taken and no fresh tile is left.  While items are in flight
+// on the XCD and none is ready the wave sleeps and polls; `spins` bounds that wait
+// (a wave that would wait ~seconds gives up rather than hang the device: the host
+// never relies on it, every item is taken by the wave that pushed it at the latest).
+__device__ int iq_next(const DecodeArgs &p, unsigned xcc, int lane, long &spins) {
+    int item = -1;
+    bool waiting = false;
+    if (lane == 0) {
+        int *c = p.iq_ctl + 32 * (xcc + 1);
+        int *ring = p.iq_ring + (long)xcc * p.iq_cap;
+        for (;;) {
+            const int taken = iq_ld(c + 2), pushed = iq_ld(c + 1);
+            if (taken < pushed) {
+                int expect = taken;
+                if (__hip_atomic_compare_exchange_strong(c + 2, &expect, taken + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    int e;
+                    long w = 0;
+                    while ((e = iq_ld(ring + taken)) == 0 && ++w < (1L << 26)) __builtin_amdgcn_s_sleep(1);   // the pusher writes it next
+                    item = e - 1;
+                    break;
+                }
+                continue;
+            }
+            if (iq_ld(p.iq_ctl) < p.n_tiles) {
+                const int f = iq_add(p.iq_ctl, 1);
+                if (f < p.n_tiles) {
+                    iq_add(c, 1);
+                    item = f * p.iters;
+                    break;
+                }
+            }
+            // no fresh tile: done once every continuation of this XCD's tiles is taken
+            if (taken >= (p.iters - 1) * iq_ld(c)) break;
+            if (++spins > (1L << 24)) break;
+            if (!waiting) {
+                iq_add(c + 3, 1);   // this XCD has a wave waiting for work
+                waiting = true;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (waiting) iq_add(c + 3, -1);
+    }
+    return __builtin_amdgcn_readfirstlane(item);
+}
+
 template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, const int *__restrict__ used,
@@ -1827,31 +1914,68 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     // taken from a queue (one atomic per tile from lane 0, issued at the tile's
     // start, consumed at its end), so waves whose codewords take longer (longer
     // merge passes) take fewer tiles and all waves finish close together.
-    for (int tile = wave; tile < p.n_tiles;) {
+    // With the item queue (p.le2t) every trip of this loop is one (tile, iteration)
+    // item from iq_next instead.  One copy of the SISO call sites serves both forms
+    // (the kernel's instruction footprint is shared by the CU's waves).
+    const bool iq = p.le2t != nullptr;
+    const unsigned xcc = iq ? (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
+    int tile = wave, it = 0, nxt = 0;
+    bool has_next = false;
+    long spins = 0;
+    for (;;) {
+        if (iq) {
+            const int item = iq_next(p, xcc, lane, spins);
+            if (item < 0) break;
+            tile = item / p.iters;
+            it = item - tile * p.iters;
+            if (it > 0) {
+                // take over the tile's Le2 from the wave of this XCD that wrote it:
+                // this CU's L1 may hold older lines of those rows
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        } else {
+            if (tile >= p.n_tiles) break;
+            if (it == 0) {
+                nxt = tile + p.n_waves;
+                if (p.tile_ctr) {
+                    int q = 0;
+                    if (lane == 0) q = atomicAdd(p.tile_ctr, 1);
+                    nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
+                }
+                has_next = nxt < p.n_tiles;
+            }
+        }
         const float *base = pro.tile_planes(tile, wave, N, buf);
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
-        int nxt = tile + p.n_waves;
-        if (p.tile_ctr) {
-            int q = 0;
-            if (lane == 0) q = atomicAdd(p.tile_ctr, 1);
-            nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
-        }
-        const bool has_next = nxt < p.n_tiles;
-        for (int it = 0; it < p.iters; ++it) {
+        double2 *L2 = iq ? p.le2t + (long)tile * NW : Le2;   // this tile's Le2 rows
+        const unsigned rs2 = iq ? (unsigned)WAVE : rs;
+        {
             progress_prio(it, p.iters);
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
             pr.hi = 2 * it < p.iters ? 3 : 1;
-            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
+            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? L2 : p.aux, inv, lane, it ? rs2 : 0u},
                                 TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
                                 lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
-            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
+            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{L2, lane, rs2}, N, ck, ring, rs, lane,
                                         sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
+        }
+        if (it < p.iters - 1) {
+            if (iq) {
+                // hand the next iteration to this XCD's queue once every Le2 store of
+                // this wave has reached the XCD's L2
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                iq_push(p, xcc, lane, tile * p.iters + it + 1);
+            } else {
+                ++it;
+            }
+            continue;
         }
         unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
         // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
@@ -1877,7 +2001,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                     const int k = min(kc + kg + u, N - 1);   // past the chunk: a valid row, unused
                     const float4 x = at(X, k * WAVE + lane);
                     xa[u] = make_float2(x.x, x.y);
-                    la[u] = at(Le2, wsrow(inv[k], rs) + lane);
+                    la[u] = at(L2, wsrow(inv[k], rs2) + lane);
                     le[u] = at(Le1, wsrow(k, rs) + lane);
                 }
 #pragma unroll
@@ -1921,7 +2045,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
             for (int k = 0; k < N; ++k) {
                 const float4 x = X[(long)k * WAVE + lane];
-                const double2 la = Le2[wsrow(inv[k], rs) + lane];
+                const double2 la = L2[wsrow(inv[k], rs2) + lane];
                 const double2 le = Le1[wsrow(k, rs) + lane];
                 const double fa = ((double)x.x + la.x) + le.x;
                 const double fb = ((double)x.y + la.y) + le.y;
@@ -1931,9 +2055,12 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         }
 #endif
         pass_mark(tepi, 4);
-        if (has_next) pro.publish();
-        buf ^= 1;
-        tile = nxt;
+        if (!iq) {
+            if (has_next) pro.publish();
+            buf ^= 1;
+            tile = nxt;
+            it = 0;
+        }
 #if TDEC_WAVE_TIMING
         ++wtiles;
 #endif

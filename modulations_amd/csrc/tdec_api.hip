@@ -1587,6 +1587,7 @@ int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes) {
     Guard g(h->device);
     if (rows > h->siso_rows) {
         quiesce(h);
+        HIPCHK(hipStreamSynchronize(h->stream));   // a flag-waited call's kernel may still be retiring
         h->pin_siso.release();   // the caller's views of the old buffer die with this call
         h->siso_rows = 0;
         // + the per-row completion flags

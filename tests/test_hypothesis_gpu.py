@@ -54,3 +54,32 @@ def test_siso_matches_oracle(n, B, scale, la_scale, sf, algo, seed):
     for b in {0, B // 2, B - 1}:
         rA, rB = O.siso(*Lc[:, b], *La[:, b], t, sf, algo=1 if algo == "log-map" else 0)
         assert np.array_equal(LeA[b], rA) and np.array_equal(LeB[b], rB), b
+
+
+@SETTINGS
+@given(n=st.integers(1, 1100), scale=st.floats(1e-3, 1e4), la_scale=st.floats(0.0, 300.0),
+       sf=st.sampled_from([0.7, 1.0]), dt=st.sampled_from(["f32", "f64", "mixed", "int"]),
+       algo=st.sampled_from(["max-log", "log-map"]), seed=st.integers(0, 2**31 - 1))
+def test_single_call_siso_dtypes_match_oracle(n, scale, la_scale, sf, dt, algo, seed):
+    """One bcjr_max_log_map call (the staged per-call path) or one-row batch
+    (log-MAP) with the channel LLRs in each dtype numba specialises on
+    (float32; float64; a mix, widened; integers), against the oracle's same
+    specialisation, every extrinsic."""
+    rng = np.random.default_rng(seed)
+    Lc = [rng.standard_normal(n) * scale + 1e-9 for _ in range(4)]
+    if dt == "f32":
+        Lc = [x.astype(np.float32) for x in Lc]
+    elif dt == "mixed":
+        Lc[1], Lc[3] = Lc[1].astype(np.float32), Lc[3].astype(np.float32)
+    elif dt == "int":
+        Lc = [np.rint(x).astype(np.int64) for x in Lc]
+    La = [rng.standard_normal(n) * la_scale for _ in range(2)]
+    if algo == "max-log":
+        LeA, LeB = M.bcjr_max_log_map(*Lc, *La, *_tabs(), n, sf)
+    else:
+        A, B = M.bcjr_max_log_map_batch(*(x[None] for x in Lc), *(x[None] for x in La), *_tabs(), n, sf, algo=algo)
+        LeA, LeB = A[0], B[0]
+    t, _ = O.trellis()
+    rA, rB = O.siso(*Lc, *La, t, sf, algo=1 if algo == "log-map" else 0)
+    np.testing.assert_array_equal(LeA, rA)
+    np.testing.assert_array_equal(LeB, rB)

@@ -212,6 +212,9 @@ int tdec_selftest(int device, int which, long long n, unsigned long long seed, l
 /* which 3 (same entry point): the log-MAP primitives outside the captured
  * tables -- every f32 t >= 48 gives 0 <= v_exp_f32(-t) <= 2^-39 (+0 at t = inf),
  * NaN -> NaN for v_exp_f32 and v_log_f32, v_log_f32(1) = 0 (n, seed ignored).
+ * which 4: the demapper's unscaled f64 division / square root (TDEC_DM_FAST64)
+ * against the compiler's sequences on n pseudo-random operands of the ranges
+ * the demapper meets (|z|, a / b, sqrt on [1, 2]).
  *
  * The exact outputs of the log-MAP primitives (the oracle's tables,
  * oracle/tdec_oracle.c orc_set_trans): out[i] = v_exp_f32(-t) (which 0) or

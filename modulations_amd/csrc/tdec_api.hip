@@ -298,6 +298,12 @@ struct ConsCache {
 };
 
 // ---- demapper -------------------------------------------------------------------------
+// compute_llr's configuration: noise_var floored at 0.005 (:202)
+static DemapCfg demap_cfg(int M, int div_f32, int sign, double noise_var, int sep) {
+    const double nv = (0.005 > noise_var) ? 0.005 : noise_var;
+    return DemapCfg{M, div_f32, sign, nv, sep, dm_nv_fast(nv)};
+}
+
 template <typename T, typename S>
 int launch_demap(int bps, const S *d_syms, long n_sym, const T *d_cons, DemapCfg c, double *d_llr,
                         hipStream_t st) {
@@ -1647,7 +1653,7 @@ int tdec_demap_dev(int device, const void *d_syms, int sym_f64, long n_sym, cons
     ConsCache &cc = *hit;
     if (int rc = cc.upload(cons, cons_f64, M, bps, f64, st)) return rc;
     DevBuf &tb = cc.buf;
-    DemapCfg c{M, div_f32, sign, (0.005 > noise_var) ? 0.005 : noise_var, cc.sep};
+    const DemapCfg c = demap_cfg(M, div_f32, sign, noise_var, cc.sep);
     if (f64) {
         if (sym_f64) return launch_demap<double, double>(bps, (const double *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
         return launch_demap<double, float>(bps, (const float *)d_syms, n_sym, (const double *)tb.p, c, d_llr, st);
@@ -1683,7 +1689,7 @@ int tdec_demap(int device, const void *syms, int sym_f64, long n_sym, const void
 }
 
 int tdec_selftest(int device, int which, long long n, unsigned long long seed, long long *mismatches) {
-    if (!mismatches || which < 0 || which > 3 || n < 0) return fail(TDEC_EINVAL, "bad selftest arguments");
+    if (!mismatches || which < 0 || which > 4 || n < 0) return fail(TDEC_EINVAL, "bad selftest arguments");
     if (which == 0) n = (1LL << 23) + 1;   // every f32 in [1, 2]
     if (which == 3) n = 0x7F800000LL - 0x42400000LL + 1;   // every f32 t in [48, +inf]
     *mismatches = 0;
@@ -1731,7 +1737,7 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;   // the table below may still be read on another stream
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
-    DemapCfg c{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep};
+    const DemapCfg c = demap_cfg(M, div_f32, -1, noise_var, h->cons.sep);
     const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
     const int chunks = (h->N + DM_KC - 1) / DM_KC;
     const long n_items = (long)n_tiles_of(B) * chunks;   // (64-codeword tile, 16-couple chunk) pairs
@@ -1923,7 +1929,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
-                      DemapCfg{M, div_f32, -1, (0.005 > noise_var) ? 0.005 : noise_var, h->cons.sep}, h->cons.buf.p};
+                      demap_cfg(M, div_f32, -1, noise_var, h->cons.sep), h->cons.buf.p};
     const dim3 grid((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL((fused_fn)k, grid, dim3(BLOCK), 0, st, a, (const int *)h->d_perm, (const int *)h->d_inv,
                        (const int *)h->d_used, fa);

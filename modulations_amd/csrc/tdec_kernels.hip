@@ -2183,28 +2183,97 @@ struct DemapCfg {
     double nv;                 // max(noise_var, 0.005) already applied (:202)
     int sep;                   // 1: separable square QAM grid (per-axis levels follow the points);
                                // 2: and each axis a Gray-labelled uniform PAM (position-ordered levels follow)
+    int nv_fast;               // nv in [2^-8, 2^16]: the unscaled f32 / f64 division (TDEC_DM_FAST64)
 };
+__host__ __device__ inline int dm_nv_fast(double nv) { return nv >= 0x1p-8 && nv <= 0x1p16; }
 // LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels in label order; for a
 // uniform grid labelled through gray[], sep == 2, + the levels in position order, 4
 // parameters and the 2 * K * 2^K neighbour positions of sym_llrs_gray)
 constexpr int DM_TAB = 768;
 
+// TDEC_DM_FAST64 (f64 tables): the compiler's own f64 division and square root
+// sequences without their range scaling, where the scaling is provably the
+// identity -- the same instructions on the same values, so the same bits:
+//   a / b: v_div_scale (identity) -> r = v_rcp_f64(b), two Newton steps
+//   r += r * (1 - b r), q = a r, rem = a - b q, q += rem r (v_div_fmas without its
+//   2^64 scale), v_div_fixup (identity for finite nonzero operands and a normal
+//   quotient); v_div_scale scales only for a denormal or huge denominator, a
+//   numerator below 2^-969, a quotient below 2^-1022 or an exponent difference
+//   >= 768;
+//   sqrt(x), x in [1, 2]: y = v_rsq_f64(x), g = x y, h = y / 2, one Goldschmidt
+//   step and two corrections (the 2^256 pre-scale applies below 2^-767 and the
+//   zero / inf class select never fires).
+// Outside those ranges the compiler's sequences run (a branch no lane takes on
+// ordinary symbols).  tdec_selftest 4 compares both against the compiler's
+// sequences on random operands over the ranges the demapper meets.
+#ifndef TDEC_DM_FAST64
+#define TDEC_DM_FAST64 1
+#endif
+// BPSK .. 16QAM (measured faster, profiles/r05/demap_ab/); the 64 / 256QAM kernels
+// keep the compiler's sequences (their registers grow past an occupancy step)
+__host__ __device__ constexpr bool dm_fast(int bps) { return TDEC_DM_FAST64 && bps <= 4; }
+// TDEC_DM_PAIRS: 16QAM's per-axis search as pair minima (sym_llrs_sep)
+#ifndef TDEC_DM_PAIRS
+#define TDEC_DM_PAIRS 1
+#endif
+__device__ __forceinline__ double rcp_nr64(double b) {   // v_div_scale-free reciprocal of the division sequence
+    double r = __builtin_amdgcn_rcp(b);
+    r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+    return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+}
+__device__ __forceinline__ double div_nr64(double a, double b, double r) {   // a / b given r = rcp_nr64(b)
+    const double q = a * r;
+    return __builtin_fma(__builtin_fma(-b, q, a), r, q);
+}
+// The f32 division the same way (v_div_scale_f32 scales for a denormal or huge
+// denominator, a numerator below 2^-104, a denormal quotient or an exponent
+// difference >= 96): r = v_rcp_f32(b), one Newton step, q = a r, two corrections
+// (the second is v_div_fmas_f32 without its scale).
+__device__ __forceinline__ float rcp_nr32(float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float div_nr32(float a, float b, float r) {   // a / b given r = rcp_nr32(b)
+    float q = a * r;
+    q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+__device__ __forceinline__ double sqrt_1_2_64(double x) {   // sqrt(x) for x in [1, 2]
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
 // One LLR from the two per-half minima (:219-225): NaN propagates, then the
 // division by the noise variance, the +-30 clip and the caller's sign.
-template <typename T> __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
+template <typename T, bool FAST = false> __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
     if (sizeof(T) == 4 && c.div_f32) {
         // the f32 quotient clipped and negated in f32: the same values as in f64
         // (f32 -> f64 is exact and so are the +-30 clip and the negation)
-        float q = (float)diff / (float)c.nv;
+        // TDEC_DM_FAST64: nv in [2^-8, 2^16], |diff| in [2^-90, 2^60]: nothing scaled
+        const float fd = (float)diff, fn = (float)c.nv, af = fabsf(fd);
+        float q = FAST && c.nv_fast && af >= 0x1p-90f && af <= 0x1p60f ? div_nr32(fd, fn, rcp_nr32(fn))
+                                                                                  : fd / fn;
         if (q == q) q = q < -30.0f ? -30.0f : (q > 30.0f ? 30.0f : q);   // np.clip(llr, -30, 30)
         return (double)(c.sign < 0 ? -q : q);
     }
-    double v = (double)diff / c.nv;
+    double v;
+    const double dd = (double)diff, ad = fabs(dd);
+    // TDEC_DM_FAST64: nv in [2^-8, 2^16] (host flag) and |diff| in [2^-900, 2^600]:
+    // no operand or quotient the division sequence would scale (zero, whose sign
+    // v_div_fixup sets, NaN and inf take the compiler's division)
+    if (FAST && c.nv_fast && ad >= 0x1p-900 && ad <= 0x1p600) v = div_nr64(dd, c.nv, rcp_nr64(c.nv));
+    else v = dd / c.nv;
     if (v == v) v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);
     return c.sign < 0 ? -v : v;
 }
-template <typename T> __device__ __forceinline__ double llr_of(T lo, T hi, const DemapCfg &c) {
-    return llr_from_diff<T>(lo - hi, c);
+template <typename T, bool FAST = false> __device__ __forceinline__ double llr_of(T lo, T hi, const DemapCfg &c) {
+    return llr_from_diff<T, FAST>(lo - hi, c);
 }
 
 // Square QAM whose label splits into K I-bits and K Q-bits (16/64/256QAM of
@@ -2237,11 +2306,28 @@ template <typename T> __device__ __forceinline__ T sqrt_1_2(T x) {
         return ru > 0.0f ? up : t;
     }
 }
-template <typename T> __device__ __forceinline__ T cabs_fin(T re, T im) {
+template <typename T, bool FAST = false> __device__ __forceinline__ T cabs_fin(T re, T im) {
     re = fabs(re);
     im = fabs(im);
     const T larger = re > im ? re : im;
     const T smaller = im < re ? im : re;
+    if constexpr (sizeof(T) == 8 && FAST) {
+        // larger in [2^-800, 2^800]: no scaling of the denominator; a numerator or
+        // quotient small enough to be scaled gives ratio < 2^-169, where
+        // fma(ratio, ratio, 1) is 1 whatever its last bits
+        if (larger >= 0x1p-800 && larger <= 0x1p800) {
+            const double ratio = div_nr64(smaller, larger, rcp_nr64(larger));
+            return sqrt_1_2_64(__builtin_fma(ratio, ratio, 1.0)) * larger;
+        }
+    }
+    if constexpr (sizeof(T) == 4 && FAST) {
+        // larger in [2^-80, 2^100]: likewise, a scaled numerator or quotient gives
+        // ratio < 2^-24 (fma(ratio, ratio, 1) = 1 in f32 below 2^-12.5)
+        if (larger >= 0x1p-80f && larger <= 0x1p100f) {
+            const float ratio = div_nr32(smaller, larger, rcp_nr32(larger));
+            return sqrt_1_2<float>(__builtin_fmaf(ratio, ratio, 1.0f)) * larger;
+        }
+    }
     const T ratio = larger != (T)0 ? smaller / larger : (T)0;
     return sqrt_1_2<T>(fma(ratio, ratio, (T)1)) * larger;
 }
@@ -2252,12 +2338,44 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
     const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
+    if constexpr (K == 2 && TDEC_DM_PAIRS) {
+        if (!(isfinite(sr) && isfinite(si))) return false;
+    }
     T all1[2], all2[2], b1[2][K][2], b2[2][K][2];   // nearest / second nearest: axis, bit-halves
     int arg[2][K][2], allarg[2];
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax) {
         const T s = ax ? si : sr;
         const T *lev = ax ? lev_q : lev_i;
+        if constexpr (K == 2 && TDEC_DM_PAIRS) {
+            // 16QAM: every bit-half holds two levels ({0, 1} / {2, 3} for the label's
+            // high bit, {0, 2} / {1, 3} for its low bit), so the streamed order
+            // statistics below are, for finite distances, a min / max / first-argmin
+            // per pair, and the axis' nearest / second nearest come from the high
+            // bit's pairs (second smallest of four = min(max of the pair minima, min
+            // of the pair maxima)) -- the same values, a third of the operations.
+            // A non-finite symbol is declined first (the streamed form declines it
+            // too: its distances are all NaN, or inf past 1.8e19).
+            T d2[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const T d = s - lev[a];
+                d2[a] = d * d;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const int p = b ? v : 2 * v, q = b ? v + 2 : 2 * v + 1;   // the half's two levels, p < q
+                    b1[ax][b][v] = fmin(d2[p], d2[q]);
+                    b2[ax][b][v] = fmax(d2[p], d2[q]);
+                    arg[ax][b][v] = d2[q] < d2[p] ? q : p;
+                }
+            all1[ax] = fmin(b1[ax][0][0], b1[ax][0][1]);
+            all2[ax] = fmin(fmax(b1[ax][0][0], b1[ax][0][1]), fmin(b2[ax][0][0], b2[ax][0][1]));
+            allarg[ax] = b1[ax][0][1] < b1[ax][0][0] ? arg[ax][0][1] : arg[ax][0][0];
+            continue;
+        }
         // streamed over the levels: nearest / second nearest of the axis and of
         // each bit-half (a NaN distance is dropped by fmin / fmax; then every
         // distance of the axis is NaN, the minima stay inf and the test below
@@ -2308,7 +2426,7 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
     // The half holding the overall nearest point has that point as its
     // candidate, so its distance is shared by every bit: BPS + 1 numpy
     // distances instead of 2 * BPS.
-    const T an = cabs_fin<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
+    const T an = cabs_fin<T, dm_fast(BPS)>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
     const T dn = an * an;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax)
@@ -2316,9 +2434,9 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
         for (int b = 0; b < K; ++b) {
             const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
             const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
-            const T a = cabs_fin<T>(sr - lev_i[ia], si - lev_q[iq]);
+            const T a = cabs_fin<T, dm_fast(BPS)>(sr - lev_i[ia], si - lev_q[iq]);
             const T ao = a * a;
-            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
+            out[ax * K + b] = llr_from_diff<T, dm_fast(BPS)>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
         }
     return true;
 }
@@ -2339,7 +2457,7 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
 #pragma unroll UNROLL
     for (int m = 0; m < M; ++m) {
         if (M > 2 && m >= c.M) break;
-        const T a = FIN ? cabs_fin<T>(sr - cons[2 * m], si - cons[2 * m + 1]) : cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
+        const T a = FIN ? cabs_fin<T, dm_fast(BPS)>(sr - cons[2 * m], si - cons[2 * m + 1]) : cabs_np<T>(sr - cons[2 * m], si - cons[2 * m + 1]);
         const T v = a * a;                     // np.abs(s - constellation) ** 2
         const bool vn = v != v;
 #pragma unroll
@@ -2355,7 +2473,7 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
     }
 #pragma unroll
     for (int b = 0; b < BPS; ++b)
-        out[b] = llr_of<T>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
+        out[b] = llr_of<T, dm_fast(BPS)>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
 }
 
 // With every lane's symbol finite (the table is), every difference is finite
@@ -2430,7 +2548,7 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
     // The half holding the overall nearest point has that point as its
     // candidate (same first-minimum rule per axis), so its distance is shared
     // by every bit: BPS + 1 numpy distances instead of 2 * BPS.
-    const T an = cabs_fin<T>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
+    const T an = cabs_fin<T, dm_fast(BPS)>(sr - lev_i[allarg[0]], si - lev_q[allarg[1]]);
     const T dn = an * an;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax)
@@ -2438,9 +2556,9 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
         for (int b = 0; b < K; ++b) {
             const int vn = (allarg[ax] >> (K - 1 - b)) & 1, vo = vn ^ 1;
             const int ia = ax ? allarg[0] : arg[0][b][vo], iq = ax ? arg[1][b][vo] : allarg[1];
-            const T a = cabs_fin<T>(sr - lev_i[ia], si - lev_q[iq]);
+            const T a = cabs_fin<T, dm_fast(BPS)>(sr - lev_i[ia], si - lev_q[iq]);
             const T ao = a * a;
-            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
+            out[ax * K + b] = llr_from_diff<T, dm_fast(BPS)>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
         }
     return true;
 }
@@ -2499,7 +2617,7 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
     }
     const T tol = eps * (2 * dmax) + tau;
     if (!(dmax < inf && gapmin > tol)) return false;
-    const T an = cabs_fin<T>(sr - pos_i[p[0]], si - pos_q[p[1]]);
+    const T an = cabs_fin<T, dm_fast(BPS)>(sr - pos_i[p[0]], si - pos_q[p[1]]);
     const T dn = an * an;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax) {
@@ -2507,10 +2625,10 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
 #pragma unroll
         for (int b = 0; b < K; ++b) {
             const int vn = (lab >> (K - 1 - b)) & 1;
-            const T a = ax ? cabs_fin<T>(sr - pos_i[p[0]], si - pos_q[cb[1][b]])
-                           : cabs_fin<T>(sr - pos_i[cb[0][b]], si - pos_q[p[1]]);
+            const T a = ax ? cabs_fin<T, dm_fast(BPS)>(sr - pos_i[p[0]], si - pos_q[cb[1][b]])
+                           : cabs_fin<T, dm_fast(BPS)>(sr - pos_i[cb[0][b]], si - pos_q[p[1]]);
             const T ao = a * a;
-            out[ax * K + b] = llr_from_diff<T>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
+            out[ax * K + b] = llr_from_diff<T, dm_fast(BPS)>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
         }
     }
     return true;
@@ -2598,7 +2716,8 @@ __global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsi
         float re = __uint_as_float((unsigned)r), im = __uint_as_float((unsigned)(r >> 32));
         if (!isfinite(re)) re = 1.5f;
         if (!isfinite(im)) im = -0.75f;
-        ok = __float_as_uint(cabs_fin<float>(re, im)) == __float_as_uint(cabs_np<float>(re, im));
+        ok = __float_as_uint(cabs_fin<float>(re, im)) == __float_as_uint(cabs_np<float>(re, im)) &&
+             __float_as_uint(cabs_fin<float, true>(re, im)) == __float_as_uint(cabs_np<float>(re, im));
     } else if (which == 3) {
         // log-MAP primitives outside the captured tables: every f32 t >= 48 (bit
         // patterns 0x42400000 .. 0x7F800000 = +inf, n ignored) gives 0 <= 2^-t <= 2^-39
@@ -2611,12 +2730,37 @@ __global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsi
             const float qn = __uint_as_float(0x7FC00000u);
             ok = ok && hw_exp2(qn) != hw_exp2(qn) && hw_log2(qn) != hw_log2(qn) && __float_as_uint(hw_log2(1.0f)) == 0u;
         }
+    } else if (which == 4) {
+        // TDEC_DM_FAST64's sequences against the compiler's on the demapper's ranges:
+        // |z| of (re, im) with exponents in [-64, 16) (a quarter of the items with
+        // |im| within a factor 2 of |re|); a / b with |a| in [2^-900, 2^600), b in
+        // [2^-8, 2^100); sqrt on [1, 2)
+        const unsigned long long r0 = splitmix64(seed + 4 * (unsigned long long)i), r1 = splitmix64(r0),
+                                 r2 = splitmix64(r1), r3 = splitmix64(r2);
+        auto mk = [](unsigned long long r, int e) {   // random sign and mantissa, exponent e
+            return __longlong_as_double((long long)((r & 0x800FFFFFFFFFFFFFull) | ((unsigned long long)(e + 1023) << 52)));
+        };
+        const int ea = (int)(r2 % 80) - 64;
+        const int eb = (r2 >> 8) & 3 ? (int)((r2 >> 16) % 80) - 64 : ea + (int)((r2 >> 24) & 1);
+        const double re = mk(r0, ea), im = mk(r1, eb);
+        ok = __double_as_longlong(cabs_fin<double, true>(re, im)) == __double_as_longlong(cabs_np<double>(re, im));
+        const double a = mk(r0, (int)(r3 % 1500) - 900), b = fabs(mk(r1, (int)((r3 >> 16) % 108) - 8));
+        ok = ok && __double_as_longlong(div_nr64(a, b, rcp_nr64(b))) == __double_as_longlong(a / b);
+        const double x = __longlong_as_double((long long)((r2 & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull));
+        ok = ok && __double_as_longlong(sqrt_1_2_64(x)) == __double_as_longlong(sqrt(x));
+        // f32: |z| with exponents in [-64, 16), a / b with |a| in [2^-90, 2^60), b in [2^-8, 2^16)
+        auto mkf = [](unsigned r, int e) { return __uint_as_float((r & 0x807FFFFFu) | ((unsigned)(e + 127) << 23)); };
+        const float fre = mkf((unsigned)r0, ea), fim = mkf((unsigned)(r0 >> 32), eb);
+        ok = ok && __float_as_uint(cabs_fin<float, true>(fre, fim)) == __float_as_uint(cabs_np<float>(fre, fim));
+        const float fa = mkf((unsigned)r1, (int)(r3 % 150) - 90), fb = fabsf(mkf((unsigned)(r1 >> 32), (int)((r3 >> 16) % 24) - 8));
+        ok = ok && __float_as_uint(div_nr32(fa, fb, rcp_nr32(fb))) == __float_as_uint(fa / fb);
     } else {
         double re = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i));
         double im = __longlong_as_double((long long)splitmix64(seed + 2 * (unsigned long long)i + 1));
         if (!isfinite(re)) re = 1.5;
         if (!isfinite(im)) im = -0.75;
-        ok = __double_as_longlong(cabs_fin<double>(re, im)) == __double_as_longlong(cabs_np<double>(re, im));
+        ok = __double_as_longlong(cabs_fin<double>(re, im)) == __double_as_longlong(cabs_np<double>(re, im)) &&
+             __double_as_longlong(cabs_fin<double, true>(re, im)) == __double_as_longlong(cabs_np<double>(re, im));
     }
     if (!ok) atomicAdd(bad, 1ull);
     const unsigned long long act = __ballot(1);   // bad[1]: items evaluated (a launch that did not run fails)
@@ -2665,6 +2809,9 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 // 1 M codewords): the table upload is not what the kernel waits on.
 #ifndef TDEC_DM_PERSIST
 #define TDEC_DM_PERSIST 0
+#endif
+#ifndef TDEC_DM_PF
+#define TDEC_DM_PF 1
 #endif
 constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
@@ -2716,21 +2863,34 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         // quotient and remainder of t by ns advance by those of BLOCK each step
         const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
         int lane = (int)threadIdx.x / ns, si = (int)threadIdx.x - lane * ns;
-        for (int t = threadIdx.x; t < WAVE * ns; t += BLOCK, lane += dq, si += dr) {
+        const int nt = WAVE * ns;
+        // the symbol of item t (lane ln, symbol sx), zero past the batch / the item's end
+        auto sym_at = [&](int t, int ln, int sx) -> float2 {
+            const long cw = tile * WAVE + ln, s = s0 + sx;
+            return t < nt && cw < B && s < S ? *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s))
+                                             : make_float2(0.0f, 0.0f);
+        };
+        // TDEC_DM_PF: the next item's symbol is loaded before this one is demapped
+        // (8PSK / 16QAM: measured faster; QPSK and 64 / 256QAM slower)
+        constexpr bool PF = TDEC_DM_PF && (BPS == 3 || BPS == 4);
+        float2 zn = PF ? sym_at((int)threadIdx.x, lane, si) : make_float2(0.0f, 0.0f);
+        for (int t = threadIdx.x; t < nt; t += BLOCK) {
+            const int ln = lane, sx = si;
+            lane += dq;
+            si += dr;
             if (si >= ns) {
                 si -= ns;
                 ++lane;
             }
-            const long cw = tile * WAVE + lane;
-            const long s = s0 + si;
+            const float2 zc = PF ? zn : sym_at(t, ln, sx);
+            if (PF) zn = sym_at(t + BLOCK, lane, si);
+            const long cw = tile * WAVE + ln;
+            const long s = s0 + sx;
             const bool live = cw < B && s < S;
             double v[BPS];
             if constexpr (SPLIT) {
                 bool dec = false;
-                if (live) {
-                    const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
-                    dec = !demap_fast<T, BPS>((T)z.x, (T)z.y, cons, c, v);
-                }
+                if (live) dec = !demap_fast<T, BPS>((T)zc.x, (T)zc.y, cons, c, v);
                 // declined symbols go to the list for k_demap_fix (which rewrites their
                 // plane entries): one atomic per wave, entries by lane rank
                 const unsigned long long m = __ballot(dec);
@@ -2749,13 +2909,12 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                 if (!live || dec) continue;
             } else {
                 if (!live) continue;
-                const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
-                demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+                demap_sym<T, BPS>((T)zc.x, (T)zc.y, cons, c, v);
             }
 #pragma unroll
             for (int b = 0; b < BPS; ++b) {
                 const long j = s * BPS + b;
-                if (j >= j0 && j < j1) L[lane * DM_LD + (int)(j - j0)] = (float)v[b];
+                if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
             }
         }
         __syncthreads();

@@ -28,14 +28,18 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mod", default="16QAM")
+    ap.add_argument("--n", type=int, default=752)
+    ap.add_argument("--rate", default="1/3")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    codec = M.DVBRCS2_Turbo(752, "1/3")
+    codec = M.DVBRCS2_Turbo(a.n, a.rate)
     B = a.batch
     info, syms, n0 = make_symbols(codec, B, a.mod, 2.0, 99, dev)
-    cons = np.ascontiguousarray(D.constellation(a.mod).astype(np.complex64))
+    # the bench's table dtype (complex128 tables demap in f64, complex64 in f32)
+    cons = np.ascontiguousarray(D.constellation(a.mod))
     bps = D.MODULATIONS[a.mod]["bps"]
-    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
+    f64, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(n0))
+    cons = np.ascontiguousarray(cons.astype(np.complex128 if f64 else np.complex64))
     tabs = T.packed_tables(codec.next_state, codec.out_W, codec.out_Y, codec.prev_state, codec.prev_input)
     pm = T.puncture_matrix(codec.punct)
     libs = [open_lib(p) for p in a.libs]
@@ -43,7 +47,7 @@ def main():
     for L in libs:
         L.tdec_planes_bytes.restype = C.c_size_t
         h = C.c_void_p()
-        assert L.tdec_create(0, 752, 1, pm.ctypes.data, 8, 0, codec.perm.ctypes.data, codec.inv_perm.ctypes.data,
+        assert L.tdec_create(0, a.n, codec.punct["period"], pm.ctypes.data, 8, 0, codec.perm.ctypes.data, codec.inv_perm.ctypes.data,
                              tabs.ctypes.data, C.byref(h)) == 0
         hs.append(h)
     nb = libs[0].tdec_planes_bytes(hs[0], B)
@@ -54,7 +58,7 @@ def main():
         for i, (L, h) in enumerate(zip(libs, hs)):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            assert L.tdec_demap_planes_dev(h, B, syms.data_ptr(), syms.shape[1], cons.ctypes.data, 0, len(cons), bps,
+            assert L.tdec_demap_planes_dev(h, B, syms.data_ptr(), syms.shape[1], cons.ctypes.data, int(f64), len(cons), bps,
                                            float(nve), int(div32), planes[i].data_ptr(), st.cuda_stream) == 0
             e1.record(st)
             torch.cuda.synchronize()
@@ -71,7 +75,7 @@ def main():
             continue
         out = (C.c_ulonglong * 8)()
         fn(out)
-        assert L.tdec_demap_planes_dev(h, B, syms.data_ptr(), syms.shape[1], cons.ctypes.data, 0, len(cons), bps,
+        assert L.tdec_demap_planes_dev(h, B, syms.data_ptr(), syms.shape[1], cons.ctypes.data, int(f64), len(cons), bps,
                                        float(nve), int(div32), pl.data_ptr(), st.cuda_stream) == 0
         fn(out)
         n = max(1, out[0])

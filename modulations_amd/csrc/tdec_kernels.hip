@@ -2251,7 +2251,21 @@ __device__ __forceinline__ double sqrt_1_2_64(double x) {   // sqrt(x) for x in 
 }
 // One LLR from the two per-half minima (:219-225): NaN propagates, then the
 // division by the noise variance, the +-30 clip and the caller's sign.
-template <typename T, bool FAST = false> __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
+// PRE: the caller has checked nv_fast and that |diff| lies in the unscaled range
+// (sym_llrs_pairs16), so the unscaled division runs without a per-LLR test.
+template <typename T, bool FAST = false, bool PRE = false>
+__device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
+    if constexpr (PRE) {
+        if (sizeof(T) == 4 && c.div_f32) {
+            const float fn = (float)c.nv;
+            float q = div_nr32((float)diff, fn, rcp_nr32(fn));
+            q = q < -30.0f ? -30.0f : (q > 30.0f ? 30.0f : q);   // finite: no NaN test
+            return (double)(c.sign < 0 ? -q : q);
+        }
+        double v = div_nr64((double)diff, c.nv, rcp_nr64(c.nv));
+        v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);
+        return c.sign < 0 ? -v : v;
+    }
     if (sizeof(T) == 4 && c.div_f32) {
         // the f32 quotient clipped and negated in f32: the same values as in f64
         // (f32 -> f64 is exact and so are the +-30 clip and the negation)
@@ -2306,7 +2320,7 @@ template <typename T> __device__ __forceinline__ T sqrt_1_2(T x) {
         return ru > 0.0f ? up : t;
     }
 }
-template <typename T, bool FAST = false> __device__ __forceinline__ T cabs_fin(T re, T im) {
+template <typename T, bool FAST = false, bool PRE = false> __device__ __forceinline__ T cabs_fin(T re, T im) {
     re = fabs(re);
     im = fabs(im);
     const T larger = re > im ? re : im;
@@ -2315,7 +2329,7 @@ template <typename T, bool FAST = false> __device__ __forceinline__ T cabs_fin(T
         // larger in [2^-800, 2^800]: no scaling of the denominator; a numerator or
         // quotient small enough to be scaled gives ratio < 2^-169, where
         // fma(ratio, ratio, 1) is 1 whatever its last bits
-        if (larger >= 0x1p-800 && larger <= 0x1p800) {
+        if (PRE || (larger >= 0x1p-800 && larger <= 0x1p800)) {
             const double ratio = div_nr64(smaller, larger, rcp_nr64(larger));
             return sqrt_1_2_64(__builtin_fma(ratio, ratio, 1.0)) * larger;
         }
@@ -2323,7 +2337,7 @@ template <typename T, bool FAST = false> __device__ __forceinline__ T cabs_fin(T
     if constexpr (sizeof(T) == 4 && FAST) {
         // larger in [2^-80, 2^100]: likewise, a scaled numerator or quotient gives
         // ratio < 2^-24 (fma(ratio, ratio, 1) = 1 in f32 below 2^-12.5)
-        if (larger >= 0x1p-80f && larger <= 0x1p100f) {
+        if (PRE || (larger >= 0x1p-80f && larger <= 0x1p100f)) {
             const float ratio = div_nr32(smaller, larger, rcp_nr32(larger));
             return sqrt_1_2<float>(__builtin_fmaf(ratio, ratio, 1.0f)) * larger;
         }
@@ -2332,14 +2346,97 @@ template <typename T, bool FAST = false> __device__ __forceinline__ T cabs_fin(T
     return sqrt_1_2<T>(fma(ratio, ratio, (T)1)) * larger;
 }
 
+// TDEC_DM_PAIRS (16QAM, nv_fast): the per-axis search below for K = 2 in closed
+// form, carrying the differences instead of level indices.  Every bit-half holds
+// two levels ({0, 1} / {2, 3} for the label's high bit, {0, 2} / {1, 3} for its
+// low bit), so its nearest / second nearest / first argmin are a min / max /
+// compare of the pair; the axis' nearest is the nearer of the high bit's pair
+// minima (ties to the lower labels, as the streamed first-minimum rule) and its
+// second nearest min(max of those minima, min of the pair maxima): the same
+// values, so the same gap test.  The candidates' differences s - level are the
+// ones the search formed (the streamed form forms them again from the indices).
+// One range test per symbol replaces the unscaled sequences' per-call tests:
+// every candidate's larger |difference| lies between the axes' nearest
+// differences and the largest difference, and every LLR numerator below twice
+// its square; a symbol outside declines (its LLRs come from the full chain).
+template <typename T>
+__device__ __forceinline__ bool sym_llrs_pairs16(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[4]) {
+    constexpr bool F32 = sizeof(T) == 4;
+    if (!(isfinite(sr) && isfinite(si))) return false;
+    const T *lev_i = cons + 2 * 16, *lev_q = lev_i + 4;
+    const T inf = (T)INFINITY;
+    const T eps = F32 ? (T)3.8e-6 : (T)7.2e-15, tau = F32 ? (T)1e-30 : (T)1e-290;
+    T dn[2], dc[2][2], all1[2];
+    bool vn[2][2];
+    T gap = inf, top = (T)0, hi = (T)0, dmax = (T)0;
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+        const T s = ax ? si : sr;
+        const T *lev = ax ? lev_q : lev_i;
+        T d[4], d2[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            d[a] = s - lev[a];
+            d2[a] = d[a] * d[a];
+            dmax = fmax(dmax, fabs(d[a]));
+        }
+        T b1[2][2], b2[2][2], bd[2][2];
+        bool lt[2][2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int p = b ? v : 2 * v, q = b ? v + 2 : 2 * v + 1;   // the half's two levels, p < q
+                lt[b][v] = d2[q] < d2[p];
+                b1[b][v] = fmin(d2[p], d2[q]);
+                b2[b][v] = fmax(d2[p], d2[q]);
+                bd[b][v] = lt[b][v] ? d[q] : d[p];
+                gap = fmin(gap, b2[b][v] - b1[b][v]);
+                top = fmax(top, b1[b][v]);
+                hi = fmax(hi, b2[b][v]);
+            }
+        const T a1 = fmin(b1[0][0], b1[0][1]), a2 = fmin(fmax(b1[0][0], b1[0][1]), fmin(b2[0][0], b2[0][1]));
+        gap = fmin(gap, a2 - a1);
+        hi = fmax(hi, a2);
+        all1[ax] = a1;
+        const bool hv = b1[0][1] < b1[0][0];                 // the nearest level's label bits
+        const bool lv = hv ? lt[0][1] : lt[0][0];
+        dn[ax] = hv ? bd[0][1] : bd[0][0];
+        dc[ax][0] = hv ? bd[0][0] : bd[0][1];               // nearest with the other high bit
+        dc[ax][1] = lv ? bd[1][0] : bd[1][1];               // nearest with the other low bit
+        vn[ax][0] = hv;
+        vn[ax][1] = lv;
+    }
+    const T tol = eps * (top + fmax(all1[0], all1[1])) + tau;
+    const T l0 = fmax(fabs(dn[0]), fabs(dn[1]));
+    if (!(hi < inf && gap > tol && l0 >= (F32 ? (T)0x1p-80f : (T)0x1p-800) && dmax <= (F32 ? (T)0x1p29f : (T)0x1p290)))
+        return false;
+    const T an = cabs_fin<T, true, true>(dn[0], dn[1]);
+    const T dq = an * an;
+    const T lo = F32 ? (c.div_f32 ? (T)0x1p-90f : (T)0x1p-149f) : (T)0x1p-900;
+    T diff[4];
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const T a = ax ? cabs_fin<T, true, true>(dn[0], dc[1][b]) : cabs_fin<T, true, true>(dc[0][b], dn[1]);
+            const T ao = a * a;
+            diff[ax * 2 + b] = vn[ax][b] ? ao - dq : dq - ao;   // m[0] - m[1], m[vn] = dn
+        }
+    if (!(fmin(fmin(fabs(diff[0]), fabs(diff[1])), fmin(fabs(diff[2]), fabs(diff[3]))) >= lo)) return false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[k] = llr_from_diff<T, true, true>(diff[k], c);
+    return true;
+}
+
 template <typename T, int BPS>
 __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr int K = BPS / 2, L = 1 << K;
     const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
-    if constexpr (K == 2 && TDEC_DM_PAIRS) {
-        if (!(isfinite(sr) && isfinite(si))) return false;
+    if constexpr (K == 2 && TDEC_DM_PAIRS && dm_fast(BPS)) {
+        if (c.nv_fast) return sym_llrs_pairs16<T>(sr, si, cons, c, out);
     }
     T all1[2], all2[2], b1[2][K][2], b2[2][K][2];   // nearest / second nearest: axis, bit-halves
     int arg[2][K][2], allarg[2];
@@ -2347,35 +2444,6 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
     for (int ax = 0; ax < 2; ++ax) {
         const T s = ax ? si : sr;
         const T *lev = ax ? lev_q : lev_i;
-        if constexpr (K == 2 && TDEC_DM_PAIRS) {
-            // 16QAM: every bit-half holds two levels ({0, 1} / {2, 3} for the label's
-            // high bit, {0, 2} / {1, 3} for its low bit), so the streamed order
-            // statistics below are, for finite distances, a min / max / first-argmin
-            // per pair, and the axis' nearest / second nearest come from the high
-            // bit's pairs (second smallest of four = min(max of the pair minima, min
-            // of the pair maxima)) -- the same values, a third of the operations.
-            // A non-finite symbol is declined first (the streamed form declines it
-            // too: its distances are all NaN, or inf past 1.8e19).
-            T d2[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const T d = s - lev[a];
-                d2[a] = d * d;
-            }
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    const int p = b ? v : 2 * v, q = b ? v + 2 : 2 * v + 1;   // the half's two levels, p < q
-                    b1[ax][b][v] = fmin(d2[p], d2[q]);
-                    b2[ax][b][v] = fmax(d2[p], d2[q]);
-                    arg[ax][b][v] = d2[q] < d2[p] ? q : p;
-                }
-            all1[ax] = fmin(b1[ax][0][0], b1[ax][0][1]);
-            all2[ax] = fmin(fmax(b1[ax][0][0], b1[ax][0][1]), fmin(b2[ax][0][0], b2[ax][0][1]));
-            allarg[ax] = b1[ax][0][1] < b1[ax][0][0] ? arg[ax][0][1] : arg[ax][0][0];
-            continue;
-        }
         // streamed over the levels: nearest / second nearest of the axis and of
         // each bit-half (a NaN distance is dropped by fmin / fmax; then every
         // distance of the axis is NaN, the minima stay inf and the test below

@@ -47,11 +47,12 @@ def _adversarial(cons, rng, shape):
     return s.reshape(shape).astype(np.complex64)
 
 
-def _check(c, syms, mod, nv):
-    cons = D.constellation(mod)
+def _check(c, syms, mod, nv, cons=None):
+    cons = D.constellation(mod) if cons is None else cons
     bps = D.MODULATIONS[mod]["bps"]
     B = syms.shape[0]
-    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, np.float64(nv))
+    nv = nv if isinstance(nv, (np.floating,)) else np.float64(nv)
+    _, div32, nve = D.demap_mode(np.complex64, cons.dtype, nv)
     c.reserve(B)
     planes = torch.empty(c.planes_bytes(B) // 4, dtype=torch.float32, device="cuda")
     c.demap_planes_device(torch.from_numpy(syms).cuda(), cons, bps, nve, planes, div_f32=div32)
@@ -125,3 +126,26 @@ def test_tables_the_fast_search_cannot_take_stay_inline(kind):
     c.depuncture_device(torch.from_numpy(ref_llr).cuda(), ref)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(planes.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["f32_division", "f64_table", "nv_outside_fast_range", "nv_floor"])
+def test_split_16qam_arithmetic_variants(case):
+    """16QAM's closed-form search and unscaled divisions (TDEC_DM_PAIRS,
+    TDEC_DM_FAST64) on every arithmetic the reference's dtypes select: the f32
+    quotient (float32 noise variance, numpy's weak scalar rule), a complex128
+    table (f64 throughout), a noise variance outside the unscaled division's
+    range (the streamed search and the compiler's division run) and the 0.005
+    floor."""
+    rng = np.random.default_rng(sum(map(ord, case)))
+    mod = "16QAM"
+    c = M.DVBRCS2_Turbo(212, "1/2")
+    S = -(-c.n_coded // 4)
+    cons = D.constellation(mod)
+    nv = {"f32_division": np.float32(0.037), "f64_table": 0.037, "nv_outside_fast_range": 1e5,
+          "nv_floor": 1e-4}[case]
+    if case == "f64_table":
+        cons = cons.astype(np.complex128)
+    syms = _adversarial(cons, rng, (70, S))
+    if case == "nv_outside_fast_range":
+        syms = (syms * 300).astype(np.complex64)
+    _check(c, syms, mod, nv, cons)

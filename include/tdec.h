@@ -114,6 +114,13 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
                            void *stream);
 int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits,
                           double *d_lfinal, void *stream);
+/* Pipelining (no reference counterpart): enqueue on `stream` a one-wave kernel
+ * that completes once h's most recent throughput decode launch (enqueued before
+ * this call, on any stream) has handed out its last tiles, so work queued after
+ * it on `stream` -- the next batch's demap -- is dispatched into the slots the
+ * decoder's retiring waves free instead of competing with the decoder's grid
+ * placement.  No-op before the first such launch; returns after ~2 s at most. */
+int tdec_tail_gate(tdec_t *h, void *stream);
 
 /* Soft demapper: compute_llr (test_sdr_with_coding.py:200-225) over any
  * labelled constellation (label i = bits MSB first).  syms: n_sym complex

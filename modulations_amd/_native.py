@@ -25,6 +25,7 @@ TDEC_OK, TDEC_EINVAL, TDEC_ESHORT, TDEC_ENOMEM, TDEC_EHIP, TDEC_EUNSUPPORTED, TD
 EXPORTS = (
     "tdec_create", "tdec_destroy", "tdec_last_error", "tdec_llr_len", "tdec_siso_batch", "tdec_decode_batch",
     "tdec_reserve", "tdec_planes_bytes", "tdec_depuncture_dev", "tdec_decode_planes_dev", "tdec_decode_batch_dev",
+    "tdec_tail_gate",
     "tdec_demap_dev", "tdec_demap", "tdec_demap_planes_dev", "tdec_encode_dev", "tdec_encoded_len",
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
     "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
@@ -64,6 +65,7 @@ def _declare(L):
     L.tdec_depuncture_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
     L.tdec_decode_planes_dev.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp]
     L.tdec_decode_batch_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp, _vp]
+    L.tdec_tail_gate.argtypes = [_vp, _vp]
     L.tdec_demap_dev.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                  C.c_int, C.c_int, _vp, _vp]
     L.tdec_demap.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,

@@ -358,6 +358,8 @@ struct tdec_ctx {
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
     int *d_tile_ctr = nullptr;         // the decoders' tile queue counter (zeroed before each launch)
+    unsigned *d_tail = nullptr;        // the throughput decoder's tail flag (DecodeArgs::tail_flag)
+    unsigned tail_seq = 0;             // sequence number of its last whole-tile launch
     int *d_simd_prog = nullptr;        // TDEC_PRIO 4 builds: per-SIMD progress slots (zeroed before each launch)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
@@ -522,6 +524,8 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMalloc(&h->d_dst, sizeof(int32_t) * dst.size());
     if (e == hipSuccess) e = hipMemcpy(h->d_dst, dst.data(), sizeof(int32_t) * dst.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&h->d_tail, sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(h->d_tail, 0, sizeof(unsigned));
     if (e == hipSuccess && TDEC_PRIO == 4) e = hipMalloc(&h->d_simd_prog, SIMD_PROG_BYTES);
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
     if (e == hipSuccess) e = hipMemcpy(h->d_off, off.data(), sizeof(int32_t) * (N + 1), hipMemcpyHostToDevice);
@@ -666,6 +670,7 @@ void tdec_destroy(tdec_t *h) {
     hipFree(h->d_decl_n);
     hipFree(h->d_decl_ovf);
     hipFree(h->d_tile_ctr);
+    hipFree(h->d_tail);
     if (h->d_simd_prog) hipFree(h->d_simd_prog);
     hipFree(h->d_off);
     if (h->ws_vmm.va) h->ws.p = nullptr;   // the VMM range is not a hipMalloc pointer
@@ -1163,6 +1168,9 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
         a.iq_ring = (int *)h->iq_ring.p;
         a.iq_cap = (int)iq_cap_of(h, tiles);
         a.tile_ctr = nullptr;
+    } else {
+        a.tail_flag = h->d_tail;
+        a.tail_seq = ++h->tail_seq;
     }
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
@@ -1170,6 +1178,16 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
                        a, pm, iv, (const int *)h->d_used);
     HIPCHK(hipGetLastError());
     return mark_used(h, st);
+}
+
+int tdec_tail_gate(tdec_t *h, void *stream) {
+    if (!h) return fail(TDEC_EINVAL, "bad tail gate arguments");
+    if (!h->tail_seq) return 0;   // no throughput launch yet: nothing to wait for
+    Guard g(h->device);
+    hipLaunchKernelGGL(k_tail_gate, dim3(1), dim3(WAVE), 0, (hipStream_t)stream, (const unsigned *)h->d_tail,
+                       h->tail_seq);
+    HIPCHK(hipGetLastError());
+    return 0;
 }
 
 int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride, int32_t *d_bits, double *d_lfinal,

@@ -1754,6 +1754,12 @@ struct DecodeArgs {
     int *iq_ctl = nullptr;
     int *iq_ring = nullptr;
     int iq_cap = 0;
+    // The launch's tail (whole-tile mode): each wave, when it takes its last tile,
+    // raises *tail_flag to tail_seq (atomicMax; seq grows per launch), which
+    // k_tail_gate waits for (tdec_tail_gate: the next batch's demap is released
+    // into the slots the retiring waves free, not before the grid is placed).
+    unsigned *tail_flag = nullptr;
+    unsigned tail_seq = 0;
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1944,6 +1950,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                     nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
                 }
                 has_next = nxt < p.n_tiles;
+                if (!has_next && p.tail_flag && lane == 0) atomicMax(p.tail_flag, p.tail_seq);
             }
         }
         const float *base = pro.tile_planes(tile, wave, N, buf);
@@ -2150,6 +2157,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_W
 
 // De-puncture (:468-487): llr rows -> tile planes X {A, B, W1, Y1} and Z {W2, Y2}.
 // src[c*N + k] = LLR index or -1 for the components c = X.xyzw, (unused, unused), Z.xy.
+// tdec_tail_gate: one wave that returns once *flag >= seq (a decoder launch has
+// handed out its last tiles), polled with agent-scope loads (the flag is raised by
+// atomics from any XCD) every ~4 us; after ~2 s it returns anyway (a late gate
+// only costs overlap, never correctness).
+__global__ __launch_bounds__(WAVE) void k_tail_gate(const unsigned *flag, unsigned seq) {
+    for (unsigned i = 0; i < (1u << 19); ++i) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= seq) return;
+        __builtin_amdgcn_s_sleep(127);
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_depuncture(int B, int N, const float *llr, long stride,
                                                      const int *__restrict__ src, float *planes, long total) {
     const long t = (long)blockIdx.x * BLOCK + threadIdx.x;

@@ -309,6 +309,11 @@ class DVBRCS2_Turbo:
                          llr.stride(0) if llr.shape[0] > 1 else llr.shape[1], _n.ptr(planes), self._stream(stream))
         return planes
 
+    def tail_gate(self, stream=None):
+        """Hold work queued after this on `stream` until this codec's latest
+        throughput decode has handed out its last tiles (tdec_tail_gate)."""
+        self.handle.call("tdec_tail_gate", self._stream(stream))
+
     def demap_planes_device(self, syms, constellation, bps, noise_var, planes, div_f32=False, stream=None):
         """Fused soft demap (decoder sign) + de-puncture of complex64 symbols [B, S]."""
         cons = np.ascontiguousarray(np.asarray(constellation))

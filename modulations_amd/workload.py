@@ -81,7 +81,7 @@ class DevicePipeline:
     needs every wave streaming to keep HBM busy.  Buffers are sized once; run()
     is stream-ordered and allocation free."""
 
-    def __init__(self, codec, mod, B, device, fused=False, overlap=False):
+    def __init__(self, codec, mod, B, device, fused=False, overlap=False, gate=True):
         import torch
         self.codec, self.mod, self.B = codec, mod, B
         self.bps = D.MODULATIONS[mod]["bps"]
@@ -111,6 +111,7 @@ class DevicePipeline:
             self.demap_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.decode_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.step = 0
+            self.gate = bool(gate)
 
     def run(self, syms, noise_var, stream=None, events=None, syms_ready=None):
         """One batch: demap -> decode, stream-ordered on `stream` (its bits are ready
@@ -131,6 +132,8 @@ class DevicePipeline:
                 sd.wait_event(syms_ready)
             else:
                 sd.wait_stream(stream)
+            if self.gate:
+                self.codec.tail_gate(sd)                # batch i-1's decode is in its tail
             self.demapper.demap_planes_device(syms, self.cons, self.bps, nve, self.planes_db[b], div_f32=div32,
                                               stream=sd)
             self.demap_done[b].record(sd)

@@ -81,7 +81,7 @@ __device__ __forceinline__ void lds_st(lds_b *p, float v) { *(lds_f1 *)p = v; }
 // ev [2][8][16] f32 segment end vectors (+ 64 B of round control), sink [2][512 B] (stores of idle groups),
 // st_a [N+1][16] f32 (alpha[k] at row k), st_b [N+1][16] (beta[k] at row k), pmt
 // [N][8] f32 pair maxima; the decoder adds p1, le2 [N] double2 and perm, inv
-// [N] int.  The recursions read up to 8 rows past pmt / st in either
+// [N] int.  The recursions read up to 16 rows past pmt / st in either
 // direction (prefetch; values unused): the arrays before st_a and the tail pad
 // keep those reads inside the allocation.
 struct FrLds {
@@ -302,6 +302,68 @@ __device__ __forceinline__ void fr_block_asm(float &v, const float (&c)[4][4], u
         : "memory");
 }
 
+// TDEC_FR_BLK8: fast blocks of 8 steps (two labelling periods) instead of 4 --
+// the same instructions per step as fr_block_asm, with the block's control
+// (run-mask and end tests, the merge compare, address updates, the next block's
+// pair-maxima loads) paid once per 8 steps.  a[ph]: LDS byte address of the
+// vector entering step ph of the block's LOWER-addressed half (alpha: steps
+// 0-3 at +0, 4-7 at +256; beta, whose rows descend: steps 0-3 at +256, 4-7 at +0),
+// c[j]: step j's own / partner pair maxima.
+#ifndef TDEC_FR_BLK8
+#define TDEC_FR_BLK8 1
+#endif
+#define FR8_STEP0(A, OFF, CO, CP, NOP)                                                          \
+    "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
+    "v_add_f32 %[u], %[v], %[" CO "]\n\t" NOP                                                 \
+    "v_add_f32_dpp %[t], %[v], %[" CP "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"            \
+    "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"                                                 \
+    "s_nop 1\n\t"                                                                             \
+    "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+#define FR8_STEP1(A, OFF, CO, CP)                                                               \
+    "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
+    "v_add_f32 %[u], %[v], %[" CO "]\n\t"                                                     \
+    "v_add_f32_dpp %[t], %[v], %[" CP "] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"            \
+    "v_add_f32_dpp %[t], %[v], %[" CP "] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"            \
+    "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"                                                 \
+    "s_nop 1\n\t"                                                                             \
+    "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+#define FR8_STEPQ(A, OFF, CO, CP, QP)                                                           \
+    "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
+    "v_add_f32 %[u], %[v], %[" CO "]\n\t"                                                     \
+    "v_add_f32_dpp %[t], %[v], %[" CP "] quad_perm:" QP " row_mask:0xf bank_mask:0xf\n\t"     \
+    "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"                                                 \
+    "s_nop 1\n\t"                                                                             \
+    "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+#define FR8_BODY(O0, O1)                                                                        \
+    FR8_STEP0("a0", O0, "c00", "c01", "s_nop 1\n\t")                                          \
+    FR8_STEP1("a1", O0, "c10", "c11")                                                         \
+    FR8_STEPQ("a2", O0, "c20", "c21", "[2,3,0,1]")                                            \
+    FR8_STEPQ("a3", O0, "c30", "c31", "[1,0,3,2]")                                            \
+    FR8_STEP0("a0", O1, "c40", "c41", "")                                                     \
+    FR8_STEP1("a1", O1, "c50", "c51")                                                         \
+    FR8_STEPQ("a2", O1, "c60", "c61", "[2,3,0,1]")                                            \
+    FR8_STEPQ("a3", O1, "c70", "c71", "[1,0,3,2]")                                            \
+    "s_nop 1"
+template <int DIR>
+__device__ __forceinline__ void fr_block8_asm(float &v, const float (&c)[8][2], unsigned a0, unsigned a1, unsigned a2,
+                                              unsigned a3) {
+    float t, u, n;
+#define FR8_OPERANDS                                                                                                  \
+    : [v] "+v"(v), [t] "=&v"(t), [u] "=&v"(u), [n] "=&v"(n)                                                          \
+    : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c00] "v"(c[0][0]), [c01] "v"(c[0][1]),                \
+      [c10] "v"(c[1][0]), [c11] "v"(c[1][1]), [c20] "v"(c[2][0]), [c21] "v"(c[2][1]), [c30] "v"(c[3][0]),            \
+      [c31] "v"(c[3][1]), [c40] "v"(c[4][0]), [c41] "v"(c[4][1]), [c50] "v"(c[5][0]), [c51] "v"(c[5][1]),            \
+      [c60] "v"(c[6][0]), [c61] "v"(c[6][1]), [c70] "v"(c[7][0]), [c71] "v"(c[7][1]), [neg] "s"(NEG)                 \
+    : "memory"
+    if constexpr (DIR == 0) asm volatile(FR8_BODY("0", "256") FR8_OPERANDS);
+    else asm volatile(FR8_BODY("256", "0") FR8_OPERANDS);
+#undef FR8_OPERANDS
+}
+#undef FR8_BODY
+#undef FR8_STEPQ
+#undef FR8_STEP1
+#undef FR8_STEP0
+
 // lanes of the 16-lane groups whose 16 bits of m are all set
 // A wave-uniform 64-bit value the compiler cannot prove uniform (it came from LDS or
 // a lane-dependent expression), moved to SGPRs: the round loop's control flow
@@ -355,7 +417,8 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
     unsigned long long reached = 0;
     float pc[4][4], pn[4][4] = {};   // per phase: the lane's own / partner pair maxima, state 0's pm[0] / pm[7]
     float cmpv = 0.0f, cmpn = 0.0f;
-    {
+    constexpr bool B8 = TDEC_FR_BLK8 && ALGO == 0 && TDEC_FR_ASMBLK && TDEC_FR_ASM && !TDEC_FR_N0 && !TDEC_FR_EXP;
+    if constexpr (!B8) {
         const lds_b *pr = R.pmt + prow(u0);
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph) {
@@ -366,8 +429,8 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
                 pc[ph][3] = lds_ld(pr + (DIR ? -32 : 32) * ph + 28);
             }
         }
-        if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
     }
+    if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
     // one block of 4 steps from pair maxima `c` while the next block's go to `n`
     // (ping-pong over two register sets: no moves between blocks)
     auto block = [&](int u, float (&c)[4][4], float (&n)[4][4], float &cv, float &cn) -> bool {
@@ -426,6 +489,66 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
         }
         return true;
     };
+    if constexpr (B8) {
+        // 8-step blocks: the pair maxima of 8 steps from the block's two row halves
+        // (alpha: rows U, U + 4 ascending; beta: its rows descend, so the lower half
+        // U + 4 is the base and U sits 4 rows above it)
+        auto load8 = [&](int U, float (&c)[8][2]) {
+            const lds_b *pb = R.pmt + prow(DIR ? U + 4 : U);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ph = j & 3, h = j >> 2, hoff = DIR ? (h ? 0 : 128) : (h ? 128 : 0);
+                c[j][0] = lds_ld(pb + hoff + L.poff[ph][0]);
+                c[j][1] = lds_ld(pb + hoff + L.poff[ph][1]);
+            }
+        };
+        auto block8 = [&](int u, float (&c)[8][2], float (&n)[8][2], float &cv, float &cn) -> bool {
+            if constexpr (CMP) run &= ~grp_all16(__ballot(v == cv));   // merged: the rest is stored already
+            if (!run) return false;
+            const int U = u0 + u;
+            load8(U + 8, n);   // the next block's (rows past the end are read, unused)
+            if constexpr (CMP) cn = lds_ld(R.st + srow(U + 8) + L.soff[0]);
+            const bool rl = (run >> lane) & 1;
+            if (!(__ballot(u + 8 >= len) & run)) {   // every running group has steps after this block
+                // idle groups store into their sink row: alpha and beta both at [0, 508)
+                lds_b *const sr = rl ? R.st + srow(DIR ? U + 4 : U) : R.sink + (DIR ? 192 : 0);
+                fr_block8_asm<DIR>(v, c, (unsigned)(uintptr_t)(sr + L.soff[0]), (unsigned)(uintptr_t)(sr + L.soff[1]),
+                                   (unsigned)(uintptr_t)(sr + L.soff[2]), (unsigned)(uintptr_t)(sr + L.soff[3]));
+            } else {   // some group ends in this block: per-step bounds, end vector captured
+                lds_b *const evg = R.ev + g * 64;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int uu = u + j;
+                    lds_b *const rw = R.st + srow(U + (j & 4));
+                    float c4[4];
+                    c4[0] = c[j][0];
+                    c4[1] = c[j][1];
+                    c4[2] = c4[3] = 0.0f;
+                    if (rl && uu < len) lds_st(rw + L.soff[j & 3], v);
+                    float vn;
+                    switch (j & 3) {
+                    case 0: vn = fr_step_a<ALGO, 0>(v, c4); break;
+                    case 1: vn = fr_step_a<ALGO, 1>(v, c4); break;
+                    case 2: vn = fr_step_a<ALGO, 2>(v, c4); break;
+                    default: vn = fr_step_a<ALGO, 3>(v, c4); break;
+                    }
+                    if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(j + 1) & 3], vn);
+                    v = vn;
+                }
+                const unsigned long long ended = __ballot(u + 8 >= len) & run;
+                reached |= ended;
+                run &= ~ended;
+            }
+            return true;
+        };
+        float qc[8][2], qn[8][2];
+        load8(u0, qc);
+        for (int u = 0;; u += 16) {
+            if (!block8(u, qc, qn, cmpv, cmpn)) break;
+            if (!block8(u + 8, qn, qc, cmpn, cmpv)) break;
+        }
+        return reached;
+    }
     for (int u = 0;; u += 8) {
         if (!block(u, pc, pn, cmpv, cmpn)) break;
         if (!block(u + 4, pn, pc, cmpn, cmpv)) break;

@@ -104,10 +104,12 @@ def lane_step(v, pm_row, ph, idx):
     return (n - n[0]).astype(np.float32)
 
 
-def frame_recursion(pm, beta, P=4, lmin=0):
+def frame_recursion(pm, beta, P=4, lmin=0, blk=8):
     """The kernel's engine: stored vectors [N][16] in step order (natural state
     order), after both passes, plus round statistics.  P segments per direction
-    (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2; 16: four waves)."""
+    (4: one wave, TDEC_FR_WPD 1; 8: two waves, TDEC_FR_WPD 2; 16: four waves);
+    a re-run compares with the stored vector at every blk-step block start
+    (8: TDEC_FR_BLK8, the default; 4: its 4-step blocks)."""
     N = pm.shape[0]
     lbl, idx = lane_consts(beta)
     Ls = max((N + 4 * P - 1) // (4 * P) * 4, lmin)      # tdec_frame.hip fr_seg_len (TDEC_FR_LMIN)
@@ -122,7 +124,7 @@ def frame_recursion(pm, beta, P=4, lmin=0):
         v = start_nat[lbl[0]].astype(np.float32)          # lane l holds state lbl[0][l]
         for u in range(ln):
             ph = u % 4
-            if cmp and ph == 0 and np.all(v == st[u0 + u][lbl[0]]):
+            if cmp and u % blk == 0 and np.all(v == st[u0 + u][lbl[0]]):
                 return False                               # merged
             st[u0 + u][lbl[ph]] = v
             k = N - 1 - (u0 + u) if beta else u0 + u
@@ -210,10 +212,11 @@ def test_lane_step_equals_serial_step(beta):
 @pytest.mark.parametrize("scale", [3.0, 1e-3])
 @pytest.mark.parametrize("P", [4, 8, 16])
 @pytest.mark.parametrize("lmin", [0, 48])
-def test_segment_rounds_equal_two_pass(beta, N, scale, P, lmin):
+@pytest.mark.parametrize("blk", [4, 8])
+def test_segment_rounds_equal_two_pass(beta, N, scale, P, lmin, blk):
     rng = np.random.default_rng(N * 3 + int(beta))
     pm = _pm(rng, N, scale)
-    st, _ = frame_recursion(pm, beta, P, lmin)
+    st, _ = frame_recursion(pm, beta, P, lmin, blk)
     np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
 
 
@@ -243,7 +246,8 @@ def test_segment_rounds_random_sweep_covers_every_path():
         if trial % 7 == 0:
             pm[rng.integers(0, N)] = np.nan
         beta = bool(trial % 2)
-        st, stats = frame_recursion(pm, beta, (4, 8, 16, 8)[trial % 4], (0, 0, 48, 32, 64)[trial % 5])
+        st, stats = frame_recursion(pm, beta, (4, 8, 16, 8)[trial % 4], (0, 0, 48, 32, 64)[trial % 5],
+                                    (8, 4)[trial % 2 if trial % 3 else 0])
         np.testing.assert_array_equal(st, reference_two_pass(pm, beta))
         seen.add((stats["spec"], stats["broken"]))
     assert {(True, False), (False, False), (False, True)} <= seen, seen

@@ -2664,6 +2664,9 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
 // each bit-half is unique and is the candidate, so the LLRs are the full scan's bit
 // for bit; anything else (non-finite input, near ties, a wrong position estimate)
 // returns false and the caller scans.
+#ifndef TDEC_DM_GRAYPRE
+#define TDEC_DM_GRAYPRE 1
+#endif
 __device__ __forceinline__ int gray_inv(int q, int K) {
     int a = q;
     for (int sh = 1; sh < K; ++sh) a ^= q >> sh;
@@ -2677,6 +2680,7 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
     int p[2], cb[2][K];
+    T e0s[2], cds[2][K];   // the nearest level's and the candidates' differences s - level
     T gapmin = inf, dmax = (T)0;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax) {
@@ -2685,6 +2689,7 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
         const T t = fmin(fmax(rint((s - prm[2 * ax]) * prm[2 * ax + 1]), (T)0), (T)(L - 1));
         const int q = (int)t;
         const T e0 = s - pos[q], d0 = e0 * e0;
+        e0s[ax] = e0;
         const T el = s - pos[q > 0 ? q - 1 : q], er = s - pos[q < L - 1 ? q + 1 : q];
         const T dl = q > 0 ? el * el : inf, dr = q < L - 1 ? er * er : inf;
         gapmin = fmin(gapmin, fmin(dl, dr) - d0);
@@ -2697,12 +2702,49 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
             const T dL = lv ? xl * xl : inf, dR = rv ? xr * xr : inf;
             if (lv && rv) gapmin = fmin(gapmin, fabs(dL - dR));
             cb[ax][b] = dL <= dR ? lc : rc;
+            cds[ax][b] = dL <= dR ? xl : xr;
             dmax = fmax(dmax, fmax(lv ? dL : (T)0, rv ? dR : (T)0));
         }
         p[ax] = q;
     }
     const T tol = eps * (2 * dmax) + tau;
     if (!(dmax < inf && gapmin > tol)) return false;
+    if constexpr (TDEC_DM_GRAYPRE) {
+        // (a noise variance outside [2^-8, 2^16] declines every symbol to the
+        // callers' other searches: the compiler's sequences below would hold their
+        // registers in this kernel too, a step of occupancy)
+        if (!c.nv_fast) return false;
+        {
+            // TDEC_DM_GRAYPRE: the differences the search formed, and one range test
+            // per symbol for the unscaled division / square root (sym_llrs_pairs16):
+            // every candidate's larger |difference| lies between the axes' nearest
+            // differences and sqrt(dmax); outside, or an LLR numerator below the
+            // quotient's range, the symbol declines to the full chain
+            constexpr bool F32 = sizeof(T) == 4;
+            const T l0 = fmax(fabs(e0s[0]), fabs(e0s[1]));
+            if (!(l0 >= (F32 ? (T)0x1p-80f : (T)0x1p-800) && dmax <= (F32 ? (T)0x1p58f : (T)0x1p580))) return false;
+            const T an = cabs_fin<T, true, true>(e0s[0], e0s[1]);
+            const T dq = an * an;
+            const T lo = F32 ? (c.div_f32 ? (T)0x1p-90f : (T)0x1p-149f) : (T)0x1p-900;
+            T diff[BPS], dlo = inf;
+#pragma unroll
+            for (int ax = 0; ax < 2; ++ax) {
+                const int lab = gray_inv(p[ax], K);
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    const int vn = (lab >> (K - 1 - b)) & 1;
+                    const T a = ax ? cabs_fin<T, true, true>(e0s[0], cds[1][b]) : cabs_fin<T, true, true>(cds[0][b], e0s[1]);
+                    const T ao = a * a;
+                    diff[ax * K + b] = vn ? ao - dq : dq - ao;   // m[0] - m[1], m[vn] = dn
+                    dlo = fmin(dlo, fabs(diff[ax * K + b]));
+                }
+            }
+            if (!(dlo >= lo)) return false;
+#pragma unroll
+            for (int k = 0; k < BPS; ++k) out[k] = llr_from_diff<T, true, true>(diff[k], c);
+            return true;
+        }
+    }
     const T an = cabs_fin<T, dm_fast(BPS)>(sr - pos_i[p[0]], si - pos_q[p[1]]);
     const T dn = an * an;
 #pragma unroll

@@ -149,3 +149,21 @@ def test_split_16qam_arithmetic_variants(case):
     if case == "nv_outside_fast_range":
         syms = (syms * 300).astype(np.complex64)
     _check(c, syms, mod, nv, cons)
+
+
+@pytest.mark.parametrize("mod", ["64QAM", "256QAM"])
+@pytest.mark.parametrize("case", ["f32_division", "f64_table", "nv_outside_fast_range"])
+def test_split_gray_arithmetic_variants(mod, case):
+    """The Gray search's pre-checked unscaled sequences (TDEC_DM_GRAYPRE) on the
+    f32 quotient, a complex128 table, and a noise variance outside their range
+    (every symbol then declines to the full chain)."""
+    rng = np.random.default_rng(sum(map(ord, mod + case)))
+    c = M.DVBRCS2_Turbo(212, "1/2")
+    bps = D.MODULATIONS[mod]["bps"]
+    S = -(-c.n_coded // bps)
+    cons = D.constellation(mod)
+    nv = {"f32_division": np.float32(0.021), "f64_table": 0.021, "nv_outside_fast_range": 1e5}[case]
+    if case == "f64_table":
+        cons = cons.astype(np.complex128)
+    syms = _adversarial(cons, rng, (66, S))
+    _check(c, syms, mod, nv, cons)

@@ -2562,6 +2562,56 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
         out[b] = llr_of<T, dm_fast(BPS)>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
 }
 
+// TDEC_DM_SCANPRE (BPSK / QPSK / 8PSK, finite symbols): the scan with the
+// unscaled division / square root under one range test per symbol instead of one
+// per point (sym_llrs_pairs16): every point's larger |difference| within [2^-80,
+// 2^29] (f32) / [2^-800, 2^290] (f64) and nv_fast, for every lane of the wave, or
+// false and the caller scans with the per-point tests.  Finite differences below
+// 2^29 give finite squares, so np.min's NaN rule never applies; an LLR numerator
+// of zero or below the quotient's range takes the compiler's division (its sign of
+// zero), per lane.
+#ifndef TDEC_DM_SCANPRE
+#define TDEC_DM_SCANPRE 0
+#endif
+template <typename T, int BPS, int M = (1 << BPS)>
+__device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
+    constexpr bool F32 = sizeof(T) == 4;
+    T dx[M], dy[M], lmin = (T)INFINITY, lmax = (T)0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const bool on = M <= 2 || m < c.M;   // a table with fewer points than 2^BPS
+        dx[m] = sr - cons[2 * m];
+        dy[m] = si - cons[2 * m + 1];
+        const T l = fmax(fabs(dx[m]), fabs(dy[m]));
+        lmin = on ? fmin(lmin, l) : lmin;
+        lmax = on ? fmax(lmax, l) : lmax;
+    }
+    const bool ok = c.nv_fast && lmin >= (F32 ? (T)0x1p-80f : (T)0x1p-800) && lmax <= (F32 ? (T)0x1p29f : (T)0x1p290);
+    if (!__all(ok)) return false;
+    T m0[BPS], m1[BPS];
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) m0[b] = m1[b] = (T)INFINITY;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        if (M > 2 && m >= c.M) break;
+        const T a = cabs_fin<T, true, true>(dx[m], dy[m]);
+        const T v = a * a;                     // np.abs(s - constellation) ** 2
+#pragma unroll
+        for (int b = 0; b < BPS; ++b) {
+            if ((m >> (BPS - 1 - b)) & 1) m1[b] = v < m1[b] ? v : m1[b];
+            else m0[b] = v < m0[b] ? v : m0[b];
+        }
+    }
+    const T lo = F32 ? (c.div_f32 ? (T)0x1p-90f : (T)0x1p-149f) : (T)0x1p-900;
+#pragma unroll
+    for (int b = 0; b < BPS; ++b) {
+        const T d = m0[b] - m1[b];
+        if (fabs(d) >= lo) out[b] = llr_from_diff<T, true, true>(d, c);
+        else out[b] = llr_from_diff<T, false>(d, c);
+    }
+    return true;
+}
+
 // With every lane's symbol finite (the table is), every difference is finite
 // and |z| is cabs_fin; BPSK / QPSK / 8PSK (M <= 8, the scan is their only
 // path) take that copy when the whole wave qualifies.
@@ -2569,6 +2619,9 @@ template <typename T, int BPS, int M = (1 << BPS)>
 __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     if constexpr (M <= 8) {
         if (__all(isfinite(sr) && isfinite(si))) {
+            if constexpr (TDEC_DM_SCANPRE && dm_fast(BPS)) {
+                if (sym_llrs_scan_pre<T, BPS>(sr, si, cons, c, out)) return;
+            }
             sym_llrs_scan<T, BPS, true>(sr, si, cons, c, out);
             return;
         }

@@ -1,0 +1,21 @@
+# (1) BPSK / QPSK / 8PSK scan with one range test per symbol (TDEC_DM_SCANPRE):
+#     demap parity + self-tests, A/B against the library without it (sp1 = with), both orders;
+# (2) configs[1] serial vs --overlap (tail gate), alternating 3 + 3.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r05x
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_selftest.py \
+  tests/test_gpu_demap_split.py tests/test_gpu_parity.py tests/test_gpu_modem.py tests/test_nonfinite.py \
+  tests/test_gpu_workload.py tests/test_gpu_fused.py > $O/tests.log 2>&1 || exit 1
+TDEC_LIB_VARIANT=sp1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_selftest.py tests/test_gpu_demap_split.py tests/test_gpu_parity.py tests/test_gpu_modem.py tests/test_nonfinite.py tests/test_gpu_workload.py tests/test_gpu_fused.py > $O/tests_sp1.log 2>&1 || exit 1
+L=modulations_amd/lib
+for m in "QPSK --n 212" "8PSK --rate 1/2"; do
+  tag=$(echo $m | cut -d' ' -f1)
+  timeout -k 10 300 python -u tools/ab_demap.py $L/libtdec.so $L/libtdec_sp1.so --mod $m --rounds 7 > $O/ab_${tag}_a.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/ab_demap.py $L/libtdec_sp1.so $L/libtdec.so --mod $m --rounds 7 > $O/ab_${tag}_b.txt 2>&1 || exit 1
+done
+for r in 1 2 3; do
+  timeout -k 10 300 python -u bench.py --no-cpu --mod QPSK --n 212 --batch 102400 --steps 20 --warmup 3 > $O/c1_serial_$r.json 2> $O/c1_serial_$r.err || exit 1
+  timeout -k 10 300 python -u bench.py --no-cpu --mod QPSK --n 212 --batch 102400 --steps 20 --warmup 3 --overlap > $O/c1_overlap_$r.json 2> $O/c1_overlap_$r.err || exit 1
+done

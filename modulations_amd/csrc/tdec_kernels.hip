@@ -2994,7 +2994,12 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_PF
 #define TDEC_DM_PF 1
 #endif
-constexpr int DM_KC = 16;                  // couples per block
+// TDEC_DM_KC: couples per block (its LDS tile [64][6 * KC + 1] f32 bounds the
+// blocks per CU: 16 -> 27.9 KB, five)
+#ifndef TDEC_DM_KC
+#define TDEC_DM_KC 16
+#endif
+constexpr int DM_KC = TDEC_DM_KC;          // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
 __host__ __device__ constexpr bool dm_split(int bps) { return TDEC_DM_SPLIT && bps >= 4 && bps % 2 == 0; }

@@ -1,4 +1,4 @@
-# Round 5 evidence, second pass (library after the flattened tile loop and the item-queue option):
+# Round 5 evidence, second pass (library after the flattened tile loop, the item-queue option and the demapper rework):
 # full GPU suite, smoke, the default bench line, per-call latencies,
 # and bench + rocprof kernel trace + PMC passes of every BASELINE config.
 set -o pipefail

@@ -1,6 +1,7 @@
 # (1) BPSK / QPSK / 8PSK scan with one range test per symbol (TDEC_DM_SCANPRE):
 #     demap parity + self-tests, A/B against the library without it (sp1 = with), both orders;
-# (2) configs[1] serial vs --overlap (tail gate), alternating 3 + 3.
+# (2) configs[1] serial vs --overlap (tail gate), alternating 3 + 3;
+# (3) couples per demap block (TDEC_DM_KC 16 / 12 / 8): LDS tile vs blocks per CU.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05x
@@ -18,4 +19,9 @@ done
 for r in 1 2 3; do
   timeout -k 10 300 python -u bench.py --no-cpu --mod QPSK --n 212 --batch 102400 --steps 20 --warmup 3 > $O/c1_serial_$r.json 2> $O/c1_serial_$r.err || exit 1
   timeout -k 10 300 python -u bench.py --no-cpu --mod QPSK --n 212 --batch 102400 --steps 20 --warmup 3 --overlap > $O/c1_overlap_$r.json 2> $O/c1_overlap_$r.err || exit 1
+done
+for m in "16QAM" "QPSK --n 212"; do
+  tag=$(echo $m | cut -d' ' -f1)
+  timeout -k 10 300 python -u tools/ab_demap.py $L/libtdec.so $L/libtdec_kc12.so $L/libtdec_kc8.so --mod $m --rounds 7 > $O/kc_${tag}_a.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/ab_demap.py $L/libtdec_kc8.so $L/libtdec_kc12.so $L/libtdec.so --mod $m --rounds 7 > $O/kc_${tag}_b.txt 2>&1 || exit 1
 done

@@ -312,6 +312,9 @@ __device__ __forceinline__ void fr_block_asm(float &v, const float (&c)[4][4], u
 #ifndef TDEC_FR_BLK8
 #define TDEC_FR_BLK8 1
 #endif
+#ifndef TDEC_FR_BLK8_LM
+#define TDEC_FR_BLK8_LM 0
+#endif
 #define FR8_STEP0(A, OFF, CO, CP, NOP)                                                          \
     "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
     "v_add_f32 %[u], %[v], %[" CO "]\n\t" NOP                                                 \
@@ -417,7 +420,9 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
     unsigned long long reached = 0;
     float pc[4][4], pn[4][4] = {};   // per phase: the lane's own / partner pair maxima, state 0's pm[0] / pm[7]
     float cmpv = 0.0f, cmpn = 0.0f;
-    constexpr bool B8 = TDEC_FR_BLK8 && ALGO == 0 && TDEC_FR_ASMBLK && TDEC_FR_ASM && !TDEC_FR_N0 && !TDEC_FR_EXP;
+    // 8-step blocks: max-log as one asm sequence, log-MAP (TDEC_FR_BLK8_LM) as C++ steps
+    constexpr bool B8 = TDEC_FR_BLK8 && !TDEC_FR_N0 && !TDEC_FR_EXP &&
+                        (ALGO == 0 ? TDEC_FR_ASMBLK && TDEC_FR_ASM : TDEC_FR_BLK8_LM != 0);
     if constexpr (!B8) {
         const lds_b *pr = R.pmt + prow(u0);
 #pragma unroll
@@ -512,8 +517,24 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
             if (!(__ballot(u + 8 >= len) & run)) {   // every running group has steps after this block
                 // idle groups store into their sink row: alpha and beta both at [0, 508)
                 lds_b *const sr = rl ? R.st + srow(DIR ? U + 4 : U) : R.sink + (DIR ? 192 : 0);
-                fr_block8_asm<DIR>(v, c, (unsigned)(uintptr_t)(sr + L.soff[0]), (unsigned)(uintptr_t)(sr + L.soff[1]),
-                                   (unsigned)(uintptr_t)(sr + L.soff[2]), (unsigned)(uintptr_t)(sr + L.soff[3]));
+                if constexpr (ALGO == 0) {
+                    fr_block8_asm<DIR>(v, c, (unsigned)(uintptr_t)(sr + L.soff[0]),
+                                       (unsigned)(uintptr_t)(sr + L.soff[1]), (unsigned)(uintptr_t)(sr + L.soff[2]),
+                                       (unsigned)(uintptr_t)(sr + L.soff[3]));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int h = j >> 2, hoff = DIR ? (h ? 0 : 256) : (h ? 256 : 0);
+                        lds_st(sr + hoff + L.soff[j & 3], v);
+                        const float c4[4] = {c[j][0], c[j][1], 0.0f, 0.0f};
+                        switch (j & 3) {
+                        case 0: v = fr_step_a<ALGO, 0>(v, c4); break;
+                        case 1: v = fr_step_a<ALGO, 1>(v, c4); break;
+                        case 2: v = fr_step_a<ALGO, 2>(v, c4); break;
+                        default: v = fr_step_a<ALGO, 3>(v, c4); break;
+                        }
+                    }
+                }
             } else {   // some group ends in this block: per-step bounds, end vector captured
                 lds_b *const evg = R.ev + g * 64;
 #pragma unroll

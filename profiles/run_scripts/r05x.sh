@@ -2,7 +2,8 @@
 #     demap parity + self-tests, A/B against the library without it (sp1 = with), both orders;
 # (2) configs[1] serial vs --overlap (tail gate), alternating 3 + 3;
 # (3) couples per demap block (TDEC_DM_KC 16 / 12 / 8): LDS tile vs blocks per CU;
-# (4) the log-MAP frame path in 8-step blocks (TDEC_FR_BLK8_LM).
+# (4) the log-MAP frame path in 8-step blocks (TDEC_FR_BLK8_LM);
+# (5) one wave per recursion direction (TDEC_FR_WPD=1) on the per-call paths.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r05x
@@ -34,6 +35,19 @@ for v in base lm8; do
   for nr in "48 1/3" "752 1/2"; do
     set -- $nr
     LAT_ALGO=log-map LAT_BATCHES=1,64 timeout -k 10 200 python tools/latency.py $1 $2 > $O/lmlat_${v}_$1_$pass.json 2>&1 || exit 1
+  done
+done
+done
+unset TDEC_LIB_VARIANT
+# (5) one wave per recursion direction (wpd1 = TDEC_FR_WPD=1: no cross-wave barriers) at small N
+TDEC_LIB_VARIANT=wpd1 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_frame.py > $O/tests_wpd1.log 2>&1 || exit 1
+for pass in 1 2; do
+for v in base wpd1; do
+  if [ $v = base ]; then unset TDEC_LIB_VARIANT; else export TDEC_LIB_VARIANT=$v; fi
+  timeout -k 10 120 python tools/siso_lat.py > $O/wsiso_${v}_$pass.json 2>&1 || exit 1
+  for nr in "48 1/3" "212 1/3" "752 1/3"; do
+    set -- $nr
+    LAT_BATCHES=1,64 timeout -k 10 200 python tools/latency.py $1 $2 > $O/wlat_${v}_$1_$pass.json 2>&1 || exit 1
   done
 done
 done

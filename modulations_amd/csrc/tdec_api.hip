@@ -1027,16 +1027,32 @@ static int frame_lds_attr(int device) {
     if (device < 0 || device >= 256) return fail(TDEC_EINVAL, "device ordinal out of range");
     std::lock_guard<std::mutex> lk(mu);
     if (done[device]) return 0;
-    const void *fns[] = {(const void *)k_turbo_decode_frame<false, 0>, (const void *)k_turbo_decode_frame<true, 0>,
-                         (const void *)k_turbo_decode_frame<false, 1>, (const void *)k_turbo_decode_frame<true, 1>,
-                         (const void *)k_siso_frame<float, 0>, (const void *)k_siso_frame<double, 0>,
-                         (const void *)k_siso_frame<float, 1>, (const void *)k_siso_frame<double, 1>};
+    const void *fns[] = {(const void *)k_turbo_decode_frame<false, 0, 1>, (const void *)k_turbo_decode_frame<true, 0, 1>,
+                         (const void *)k_turbo_decode_frame<false, 1, 1>, (const void *)k_turbo_decode_frame<true, 1, 1>,
+                         (const void *)k_siso_frame<float, 0, 1>, (const void *)k_siso_frame<double, 0, 1>,
+                         (const void *)k_siso_frame<float, 1, 1>, (const void *)k_siso_frame<double, 1, 1>,
+                         (const void *)k_turbo_decode_frame<false, 0, 2>, (const void *)k_turbo_decode_frame<true, 0, 2>,
+                         (const void *)k_turbo_decode_frame<false, 1, 2>, (const void *)k_turbo_decode_frame<true, 1, 2>,
+                         (const void *)k_siso_frame<float, 0, 2>, (const void *)k_siso_frame<double, 0, 2>,
+                         (const void *)k_siso_frame<float, 1, 2>, (const void *)k_siso_frame<double, 1, 2>};
     for (const void *f : fns) {
         const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, FR_LDS_MAX);
         if (r != hipSuccess) return fail(TDEC_EHIP, std::string("hipFuncSetAttribute (frame decoder LDS): ") + hipGetErrorString(r));
     }
     done[device] = 1;
     return 0;
+}
+
+// Waves per recursion direction of the frame kernels, by block length: one wave
+// (segments and rounds inside it, no cross-wave barriers) up to fr_wpd1_max, two
+// above (8 segments: shorter chains once N is long).  Measured (profiles/r05/wpd/):
+// decode() per frame N = 48 0.132 -> 0.118 ms, 212 0.189 -> 0.149, 752 0.200 ->
+// 0.248 (worse); one SISO call 0.024 -> 0.021, 0.037 -> 0.029, 0.038 -> 0.035.
+// TDEC_FR_WPD1_MAX / TDEC_FR_SISO_WPD1_MAX override the limits (read per call).
+static int fr_wpd(int N, bool siso) {
+    const char *e = getenv(siso ? "TDEC_FR_SISO_WPD1_MAX" : "TDEC_FR_WPD1_MAX");
+    const int lim = e ? atoi(e) : (siso ? 1 << 30 : 424);
+    return N <= lim ? 1 : 2;
 }
 
 static int ensure_lowlat(tdec_t *h, int B) {
@@ -1139,8 +1155,11 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
             const bool lg = frame_le2_global(h->N);
             FrArgs a{B, h->N, h->iters, d_planes, (double2 *)h->ll_ws.p, d_bits, d_lfinal, h->n_used,
                      lg ? (double2 *)h->ll_ws.p + (size_t)B * h->N : nullptr};
-            const auto kern = h->algo ? (lg ? k_turbo_decode_frame<true, 1> : k_turbo_decode_frame<false, 1>)
-                                      : (lg ? k_turbo_decode_frame<true, 0> : k_turbo_decode_frame<false, 0>);
+            const bool w1 = fr_wpd(h->N, false) == 1;
+            const auto kern = h->algo ? (lg ? (w1 ? k_turbo_decode_frame<true, 1, 1> : k_turbo_decode_frame<true, 1, 2>)
+                                            : (w1 ? k_turbo_decode_frame<false, 1, 1> : k_turbo_decode_frame<false, 1, 2>))
+                                      : (lg ? (w1 ? k_turbo_decode_frame<true, 0, 1> : k_turbo_decode_frame<true, 0, 2>)
+                                            : (w1 ? k_turbo_decode_frame<false, 0, 1> : k_turbo_decode_frame<false, 0, 2>));
             hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(FR_BLOCK), fr_lds(h->N, true, lg).total, st, a,
                                (const int *)h->d_perm, (const int *)h->d_inv, (const int *)h->d_ford);
             HIPCHK(hipGetLastError());
@@ -1407,8 +1426,10 @@ static int siso_launch(tdec_t *h, int n, const T *A, const T *B, const T *W, con
     constexpr bool F64 = sizeof(T) == 8;
     if (fr) {
         FrSisoArgs fa{n, h->N, A, B, W, Y, la, lb, sf, ea, eb, done, h->siso_seq};
-        hipLaunchKernelGGL((h->algo ? k_siso_frame<T, 1> : k_siso_frame<T, 0>), dim3((unsigned)n), dim3(FR_BLOCK),
-                           fr_lds(h->N, false).total, s, fa);
+        const bool w1 = fr_wpd(h->N, true) == 1;
+        hipLaunchKernelGGL((h->algo ? (w1 ? k_siso_frame<T, 1, 1> : k_siso_frame<T, 1, 2>)
+                                    : (w1 ? k_siso_frame<T, 0, 1> : k_siso_frame<T, 0, 2>)),
+                           dim3((unsigned)n), dim3(FR_BLOCK), fr_lds(h->N, false).total, s, fa);
         HIPCHK(hipGetLastError());
         return 0;
     }
@@ -1757,8 +1778,8 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
     const DemapCfg c = demap_cfg(M, div_f32, -1, noise_var, h->cons.sep);
     const long n_avail = std::min<long>((long)S * bps, h->llr_len);   // LLRs the symbols provide
-    const int chunks = (h->N + DM_KC - 1) / DM_KC;
-    const long n_items = (long)n_tiles_of(B) * chunks;   // (64-codeword tile, 16-couple chunk) pairs
+    const int chunks = (h->N + dm_kc(bps) - 1) / dm_kc(bps);
+    const long n_items = (long)n_tiles_of(B) * chunks;   // (64-codeword tile, dm_kc-couple chunk) pairs
     float *P = d_planes;
     const long n_tiles = n_tiles_of(B);
     DemapDecl dd{h->d_decl, h->d_decl_n, h->d_decl_ovf, DM_DECL_CAP};

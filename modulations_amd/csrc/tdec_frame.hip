@@ -312,8 +312,11 @@ __device__ __forceinline__ void fr_block_asm(float &v, const float (&c)[4][4], u
 #ifndef TDEC_FR_BLK8
 #define TDEC_FR_BLK8 1
 #endif
+// TDEC_FR_BLK8_LM: the log-MAP recursion in the same 8-step blocks, as C++ steps
+// (profiles/r05/frame_lm8/: log-MAP decode() per frame N = 752 r = 1/2 1.085 ->
+// 0.916 ms, N = 48 0.200 -> 0.178 ms; same bits)
 #ifndef TDEC_FR_BLK8_LM
-#define TDEC_FR_BLK8_LM 0
+#define TDEC_FR_BLK8_LM 1
 #endif
 #define FR8_STEP0(A, OFF, CO, CP, NOP)                                                          \
     "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
@@ -880,7 +883,7 @@ struct FrOutRow {
 
 // One SISO (:116-281) of the workgroup's codeword.  pos[j]: this thread's positions
 // (-1: none), raw[j] their channel values.  Ends with a barrier.
-template <int ALGO, class In, class Out>
+template <int ALGO, int WPD, class In, class Out>
 __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], const typename In::Raw (&raw)[FR_J],
                         lds_b *sm, const FrLds &Lo, int N, double sf) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -909,7 +912,7 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
     // R: alpha on wave 0, beta on wave 1 (TDEC_FR_WPD 2: alpha on waves 0-1, beta on 2-3)
-    if constexpr (TDEC_FR_WPD == 1) {
+    if constexpr (WPD == 1) {
         if (wave == 0) fr_recursion<0, ALGO>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
         else if (wave == 1) fr_recursion<1, ALGO>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N}, lane);
     } else {
@@ -965,8 +968,10 @@ struct FrArgs {
 
 // DVBRCS2_Turbo.decode (:464-537) of one codeword per workgroup (grid = B).
 // ord: [N] the positions in perm's image (ascending), then the others.
-// LG: Le2 in global scratch (N > 805; see fr_lds).
-template <bool LG, int ALGO = 0>
+// LG: Le2 in global scratch (N > 805; see fr_lds).  WPD: waves per recursion
+// direction (1: one wave, segments and rounds inside it, no cross-wave barriers;
+// 2: fr_recursion_x), chosen per call by N (tdec_api.hip fr_wpd).
+template <bool LG, int ALGO = 0, int WPD = TDEC_FR_WPD>
 __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
                                                                  const int *__restrict__ inv,
                                                                  const int *__restrict__ ord) {
@@ -1007,12 +1012,12 @@ __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const
         const double sf = it < p.iters - 1 ? 0.7 : 1.0;   // :496
         const bool last = it == p.iters - 1;
         if constexpr (LG) {
-            fr_siso<ALGO>(FrIn1T<const double2 *>{le2g, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos,
+            fr_siso<ALGO, WPD>(FrIn1T<const double2 *>{le2g, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos,
                           xr, sm, Lo, N, sf);
-            fr_siso<ALGO>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<double2 *>{le2g}, pos, zr, sm, Lo, N, sf);
+            fr_siso<ALGO, WPD>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<double2 *>{le2g}, pos, zr, sm, Lo, N, sf);
         } else {
-            fr_siso<ALGO>(FrIn1{le2s, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
-            fr_siso<ALGO>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<lds_d2 *>{le2s}, pos, zr, sm, Lo, N, sf);
+            fr_siso<ALGO, WPD>(FrIn1{le2s, sinv}, FrOut1{sm + Lo.p1, last ? le1 : nullptr, p.n_used}, pos, xr, sm, Lo, N, sf);
+            fr_siso<ALGO, WPD>(FrIn2{sm + Lo.p1, sperm}, FrOut2T<lds_d2 *>{le2s}, pos, zr, sm, Lo, N, sf);
         }
     }
     // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
@@ -1047,7 +1052,8 @@ struct FrSisoArgs {
     unsigned *done;   // nullable: host-mapped per-row completion flags, set to seq after the row's outputs
     unsigned seq;
 };
-template <typename T, int ALGO = 0> __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
+template <typename T, int ALGO = 0, int WPD = TDEC_FR_WPD>
+__global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;
     const long row = (long)blockIdx.x * p.N;
@@ -1061,7 +1067,7 @@ template <typename T, int ALGO = 0> __global__ __launch_bounds__(FR_BLOCK) void 
         pos[j] = i < p.N ? i : -1;
         raw[j] = in.fetch(i < p.N ? i : 0);
     }
-    fr_siso<ALGO>(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
+    fr_siso<ALGO, WPD>(in, FrOutRow{p.LeA + row, p.LeB + row}, pos, raw, sm, fr_lds(p.N, false), p.N, p.sf);
     if (p.done) {
         // every thread's extrinsic stores are system-visible before the row's flag:
         // the host polls the flags instead of waiting for the kernel's end

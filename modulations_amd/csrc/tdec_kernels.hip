@@ -2569,9 +2569,10 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
 // false and the caller scans with the per-point tests.  Finite differences below
 // 2^29 give finite squares, so np.min's NaN rule never applies; an LLR numerator
 // of zero or below the quotient's range takes the compiler's division (its sign of
-// zero), per lane.
+// zero), per lane.  Measured (profiles/r05/demap_scan/, same planes): 8PSK
+// 12.66 -> 11.61 ms, QPSK 5.88 -> 5.70 ms per 1 M codewords.
 #ifndef TDEC_DM_SCANPRE
-#define TDEC_DM_SCANPRE 0
+#define TDEC_DM_SCANPRE 1
 #endif
 template <typename T, int BPS, int M = (1 << BPS)>
 __device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
@@ -2999,9 +3000,17 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_KC
 #define TDEC_DM_KC 16
 #endif
+// TDEC_DM_KC_QPSK: QPSK's (its kernel is LDS-bound at five blocks per CU, and its
+// work per block small: 12 couples measured faster, 5.47 vs 5.82 ms per 1 M N = 212
+// codewords; 16QAM slower with 12 or 8, 13.45 / 13.41 vs 12.75 ms,
+// profiles/r05/demap_kc/)
+#ifndef TDEC_DM_KC_QPSK
+#define TDEC_DM_KC_QPSK 12
+#endif
 constexpr int DM_KC = TDEC_DM_KC;          // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
+__host__ __device__ constexpr int dm_kc(int bps) { return bps == 2 ? TDEC_DM_KC_QPSK : TDEC_DM_KC; }
 __host__ __device__ constexpr bool dm_split(int bps) { return TDEC_DM_SPLIT && bps >= 4 && bps % 2 == 0; }
 
 // The decline list of k_demap_planes (TDEC_DM_SPLIT): entries {codeword, symbol},
@@ -3033,15 +3042,16 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                                                        const int *__restrict__ off, long n_avail, float *planes,
                                                        long n_items, DemapDecl dd) {
     __shared__ T cons[DM_TAB];
-    __shared__ float L[WAVE * DM_LD];
+    constexpr int KC = dm_kc(BPS), LD = 6 * KC + 1;   // couples per item, LDS row stride (odd)
+    __shared__ float L[WAVE * LD];
     static_assert(!SPLIT || dm_split(BPS), "split only for square 16 / 64 / 256QAM");
     load_table<T, BPS>(cons, cons_g, c);
-    const int chunks = (N + DM_KC - 1) / DM_KC;
+    const int chunks = (N + KC - 1) / KC;
     __syncthreads();
     for (long item = blockIdx.x; item < n_items; item += gridDim.x) {
         const long tile = item / chunks;
-        const int k0 = (int)(item % chunks) * DM_KC;
-        const int k1 = min(N, k0 + DM_KC);
+        const int k0 = (int)(item % chunks) * KC;
+        const int k1 = min(N, k0 + KC);
         const long j0 = off[k0], j1 = off[k1];
         const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
         const int ns = (int)(s1 - s0);
@@ -3100,7 +3110,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
 #pragma unroll
             for (int b = 0; b < BPS; ++b) {
                 const long j = s * BPS + b;
-                if (j >= j0 && j < j1) L[ln * DM_LD + (int)(j - j0)] = (float)v[b];
+                if (j >= j0 && j < j1) L[ln * LD + (int)(j - j0)] = (float)v[b];
             }
         }
         __syncthreads();
@@ -3116,7 +3126,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             for (int cc = 0; cc < 4; ++cc) {
                 if (cc >= nc) break;
                 const int j = src[(long)(half ? 6 + cc : cc) * N + k];
-                v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * DM_LD + (int)(j - j0)] : 0.0f;
+                v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + (int)(j - j0)] : 0.0f;
             }
             if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
             else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);

@@ -54,23 +54,24 @@ constexpr int FR_BLOCK = FR_WAVES * WAVE;
 #define TDEC_FR_WPD 2
 #endif
 constexpr int FR_NSEG_MAX = TDEC_FR_WPD == 4 ? 16 : 8;   // segments per direction at most
-// TDEC_FR_LMIN: the shortest segment (steps, a multiple of 4).  A segment shorter
-// than the recursions' typical merge depth (~40 steps) rarely merges in its first
-// re-run, so the rounds hand end vectors down a chain of segments: at N = 48 the
-// even split (8-step segments) made every SISO ~17 us of rounds and barriers where
-// one 48-step segment is two serial passes.  Measured (profiles/r05c/, host-pointer
-// calls, medians of two passes; segments of at least 0 / 32 / 48 / 64 / 96 steps):
-// decode() per frame N = 48: 0.291 / 0.183 / 0.148 / 0.147 / 0.148 ms; N = 212: 0.235 /
-// 0.223 / 0.207 / 0.217 / 0.239 ms; N = 752 unchanged (96-step segments either way);
-// bcjr_max_log_map N = 48: 0.041 / 0.033 / 0.029 / 0.029 / 0.029 ms.
+// TDEC_FR_LMIN: segments per direction = N / TDEC_FR_LMIN (at least 1, at most the
+// P the waves provide), the steps split evenly over them in whole 4-step blocks.
+// A segment shorter than the recursions' typical merge depth (~40 steps) rarely
+// merges in its first re-run, so the rounds hand end vectors down a chain of
+// segments: at N = 48 the even split (8-step segments) made every SISO ~17 us of
+// rounds and barriers where one 48-step segment is two serial passes (round 5's
+// first rule, a floor of 48 steps, profiles/r05c/: decode() per frame N = 48 0.291 ->
+// 0.148 ms).  The floor left N = 64 as 48 + 16 steps; splitting evenly with at
+// least 32 steps per segment gives 32 + 32 (one wave per direction,
+// profiles/r05/lmin_wpd1/: N = 64 0.150 -> 0.123 ms) and the same segments at
+// every other block size.
 #ifndef TDEC_FR_LMIN
-#define TDEC_FR_LMIN 48
+#define TDEC_FR_LMIN 32
 #endif
-// segment length of a direction split over P segments: N / P rounded up to whole
-// 4-step blocks, at least TDEC_FR_LMIN
 __host__ __device__ constexpr int fr_seg_len(int N, int P) {
-    const int L = (N + 4 * P - 1) / (4 * P) * 4;
-    return L > TDEC_FR_LMIN ? L : TDEC_FR_LMIN;
+    int n = N / TDEC_FR_LMIN;
+    n = n < 1 ? 1 : (n > P ? P : n);
+    return (N + 4 * n - 1) / (4 * n) * 4;
 }
 typedef __attribute__((address_space(3))) char lds_b;   // byte-addressed LDS
 

@@ -112,7 +112,8 @@ def frame_recursion(pm, beta, P=4, lmin=0, blk=8):
     (8: TDEC_FR_BLK8, the default; 4: its 4-step blocks)."""
     N = pm.shape[0]
     lbl, idx = lane_consts(beta)
-    Ls = max((N + 4 * P - 1) // (4 * P) * 4, lmin)      # tdec_frame.hip fr_seg_len (TDEC_FR_LMIN)
+    n = P if lmin == 0 else min(P, max(1, N // lmin))   # tdec_frame.hip fr_seg_len (TDEC_FR_LMIN)
+    Ls = (N + 4 * n - 1) // (4 * n) * 4
     nseg = (N + Ls - 1) // Ls
     seg = [(g * Ls, max(0, min(Ls, N - g * Ls))) for g in range(P)]
     st = np.full((N, 16), np.nan, np.float32)
@@ -211,7 +212,7 @@ def test_lane_step_equals_serial_step(beta):
 @pytest.mark.parametrize("N", [1, 2, 3, 5, 8, 13, 16, 17, 33, 48, 101, 212])
 @pytest.mark.parametrize("scale", [3.0, 1e-3])
 @pytest.mark.parametrize("P", [4, 8, 16])
-@pytest.mark.parametrize("lmin", [0, 48])
+@pytest.mark.parametrize("lmin", [0, 32, 48])
 @pytest.mark.parametrize("blk", [4, 8])
 def test_segment_rounds_equal_two_pass(beta, N, scale, P, lmin, blk):
     rng = np.random.default_rng(N * 3 + int(beta))

@@ -967,8 +967,8 @@ placed:
 // decoder.  TDEC_LOWLAT_MAX overrides the threshold (0 disables it).
 // Round 4, the frame decoder against the throughput decoder (host-pointer calls,
 // profiles/r04u/): N = 752 r = 1/2 B = 8 192 16.3 vs 19.7 ms, 16 384 32.9 vs 26.7 ms;
-// N = 212 B = 4 096 4.3 vs 5.6 ms, 8 192 8.5 vs 6.2 ms: the threshold is 8 192 for
-// N >= 400 and 4 096 below.
+// N = 212 B = 4 096 4.3 vs 5.6 ms, 8 192 8.5 vs 6.2 ms: the threshold was 8 192 for
+// N >= 400 and 4 096 below (round 5: 12 288 / 8 192, below).
 static size_t ll_lds_bytes(int N) { return 3 * sizeof(int) * (size_t)N; }   // perm, inv_perm, used list
 // The frame decoder (tdec_frame.hip, one codeword per workgroup, everything in
 // LDS) takes the small batches when its LDS fits (N <= 805: every BASELINE
@@ -998,9 +998,13 @@ static int lowlat_max(const tdec_t *h) {
         return v >= 0 ? v : LM_FRAME_MAX;
     }
     if (v >= 0) return v;
-    // 8 192 was measured for the frame decoder only; the state-per-lane decoder's
-    // own crossover is 4 096 (26.1 vs 20.2 ms at 8 192, profiles/r03llmax/)
-    return h->N >= 400 && use_frame_decoder(h) ? 8192 : 4096;
+    // the state-per-lane decoder's own crossover is 4 096 (26.1 vs 20.2 ms at 8 192,
+    // profiles/r03llmax/).  The frame decoder's, re-measured after round 5's frame
+    // speedups (profiles/r05/crossover/, host-pointer decode_batch, frame vs
+    // throughput decoder): N = 752 B = 8 192 13.5 vs 18.6 ms, 12 288 19.7 vs 22.7,
+    // 16 384 26.3 vs 26.1; N = 212 B = 8 192 5.7 vs 6.1 ms, 12 288 8.4 vs 6.7
+    if (!use_frame_decoder(h)) return 4096;
+    return h->N >= 400 ? 12288 : 8192;
 }
 // One predicate for "the small-batch decoders can run on this handle" (reserve and decode).
 static bool lowlat_usable(const tdec_t *h) {

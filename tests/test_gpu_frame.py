@@ -164,12 +164,12 @@ def test_frame_decode_n848_batches_and_lfinal_every_row():
         np.testing.assert_array_equal(lf, rl)
 
 
-def test_frame_decode_at_the_routing_threshold():
-    """8 192 codewords at N = 752 (the frame decoder's batch limit for N >= 400,
-    tdec_api.hip lowlat_max): 8 192 workgroups, the largest batch it serves."""
-    rng = np.random.default_rng(8192)
-    c = M.DVBRCS2_Turbo(752, "1/2")
-    B = 8192
+@pytest.mark.parametrize("n,rate,B", [(752, "1/2", 12288), (212, "1/3", 8192)])
+def test_frame_decode_at_the_routing_threshold(n, rate, B):
+    """The frame decoder's batch limits (tdec_api.hip lowlat_max: 12 288 codewords
+    for N >= 400, 8 192 below): the largest batches it serves, one workgroup each."""
+    rng = np.random.default_rng(B + n)
+    c = M.DVBRCS2_Turbo(n, rate)
     base = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in rng.integers(0, 2, (64, c.k_info))])
     llr = (base[rng.integers(0, 64, B)] + rng.standard_normal((B, c.n_coded)) * 1.6).astype(np.float32)
     bits, lf = c.decode_batch(llr, return_lfinal=True)

@@ -111,8 +111,9 @@ def test_throughput_decoder_at_small_batches(n, rate):
 
 @pytest.mark.parametrize("n,rate,interleaver", [(212, "1/3", "reference"), (752, "1/2", "valid-perm")])
 def test_lowlat_large_batch_matches_oracle(n, rate, interleaver):
-    """B above the 2 048 resident waves (the default crossover is 4 096): more than
-    one round of one-wave blocks; with a true permutation every position is in
+    """B above the 2 048 resident waves (below the small-batch limit, 8 192 / 12 288
+    for the frame decoder, 4 096 for the state-per-lane one): more than one round of
+    small-batch blocks; with a true permutation every position is in
     perm's image, so decoder 1 computes every extrinsic (the used-position list
     is the identity)."""
     rng = np.random.default_rng(77 + n)

@@ -987,7 +987,10 @@ static bool use_frame_decoder(const tdec_t *h) {
 // (profiles/r05/logmap_frame/, N = 752 r = 1/2, host-pointer calls): frame decoder
 // 1.08 / 1.32 / 5.30 / 20.4 / 43.1 ms at B = 1 / 64 / 1 024 / 4 096 / 8 192, the
 // throughput kernel 27.9 / 28.0 / 28.7 / 30.0 / 34.4 ms: the crossover is near 6 000.
-constexpr int LM_FRAME_MAX = 6144;
+// After the 8-step log-MAP frame blocks (profiles/r05/crossover_lm/): N = 752 r = 1/2
+// frame 28.4 / 37.0 ms at B = 6 144 / 8 192 against 33.3 / 34.5, N = 212 7.9 / 10.6
+// against 9.6 / 9.7: near 7 000 for both.
+constexpr int LM_FRAME_MAX = 7168;
 static int lowlat_max(const tdec_t *h) {
     static const int v = [] {
         const char *e = getenv("TDEC_LOWLAT_MAX");

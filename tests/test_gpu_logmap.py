@@ -181,13 +181,13 @@ def test_logmap_frame_decode_edge_inputs(kind):
 
 
 def test_logmap_frame_equals_throughput_decoder():
-    """4 096 codewords through the frame decoder, 6 145 (one more than its limit,
+    """4 096 codewords through the frame decoder, 7 169 (one more than its limit,
     tdec_api.hip LM_FRAME_MAX) through the persistent throughput kernel: the same
     bits on the shared rows."""
     rng = np.random.default_rng(4097)
     c = M.DVBRCS2_Turbo(752, "1/2", algo="log-map")
     base = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in rng.integers(0, 2, (32, c.k_info))])
-    llr = (base[rng.integers(0, 32, 6145)] + rng.standard_normal((6145, c.n_coded)) * 1.5).astype(np.float32)
+    llr = (base[rng.integers(0, 32, 7169)] + rng.standard_normal((7169, c.n_coded)) * 1.5).astype(np.float32)
     b_frame, l_frame = c.decode_batch(llr[:4096], return_lfinal=True)
     b_tp, l_tp = c.decode_batch(llr, return_lfinal=True)
     assert np.array_equal(b_frame, b_tp[:4096])

@@ -57,6 +57,21 @@ def test_frame_siso_matches_oracle(n, sf):
     _check_siso(Lc, La, n, sf)
 
 
+@pytest.mark.parametrize("wpd", ["one", "two"])
+def test_frame_siso_every_length_to_160(wpd, monkeypatch):
+    """Every N from 1 to 160 (segments per direction N / 32, split evenly in whole
+    4-step blocks, ragged last blocks, 8-step fast blocks and their per-step tail)
+    on both recursion layouts (TDEC_FR_SISO_WPD1_MAX: one wave per direction, or
+    two), at a low a-priori scale so merges come late and rounds hand end vectors
+    down the chain."""
+    if wpd == "two":
+        monkeypatch.setenv("TDEC_FR_SISO_WPD1_MAX", "0")
+    rng = np.random.default_rng(160)
+    for n in range(1, 161):
+        Lc, La = _siso_inputs(rng, 2, n, 1.0, 1.0)
+        _check_siso(Lc, La, n, 0.7)
+
+
 def test_frame_siso_single_row_is_the_drop_in():
     rng = np.random.default_rng(3)
     n = 752
@@ -110,6 +125,26 @@ def test_frame_decode_matches_oracle(n, rate, B, noise):
     info = rng.integers(0, 2, (B, c.k_info))
     llr = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in info]).astype(np.float32)
     llr += (rng.standard_normal(llr.shape) * noise).astype(np.float32)
+    bits, lf = c.decode_batch(llr, return_lfinal=True)
+    rb, rl = O.decode_batch(llr, c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
+                            c.inv_perm, TAB, want_lfinal=True, nthreads=8)
+    assert np.array_equal(bits, rb)
+    np.testing.assert_array_equal(lf, rl)
+
+
+@pytest.mark.parametrize("n,rate", [(48, "1/3"), (212, "1/3"), (424, "1/2"), (752, "1/3"), (848, "1/3")])
+@pytest.mark.parametrize("layout", ["one", "two"])
+def test_frame_decode_both_recursion_layouts(n, rate, layout, monkeypatch):
+    """The decoder with one wave per recursion direction and with two, at every
+    block size, whatever tdec_api.hip fr_wpd would pick (TDEC_FR_WPD1_MAX, read per
+    call): the same bits and L_final as the oracle."""
+    monkeypatch.setenv("TDEC_FR_WPD1_MAX", "100000" if layout == "one" else "0")
+    rng = np.random.default_rng(n + 7)
+    c = M.DVBRCS2_Turbo(n, rate)
+    B = 33
+    info = rng.integers(0, 2, (B, c.k_info))
+    llr = np.stack([(1 - 2.0 * c.encode(b)) * 2.0 for b in info]).astype(np.float32)
+    llr += (rng.standard_normal(llr.shape) * 1.7).astype(np.float32)
     bits, lf = c.decode_batch(llr, return_lfinal=True)
     rb, rl = O.decode_batch(llr, c.N, c.punct["period"], T.puncture_matrix(c.punct), c.iterations, c.perm,
                             c.inv_perm, TAB, want_lfinal=True, nthreads=8)

@@ -107,16 +107,9 @@ struct VmmBuf {
             return fail(TDEC_ENOMEM, "hipMemAddressReserve failed");
         }
         h.resize(n);
+        dev = device;
         std::vector<size_t> order(n);
-        for (size_t i = 0; i < n; ++i) order[i] = i;
-        unsigned long long x = 0x9E3779B97F4A7C15ull ^ seed;   // splitmix shuffle (deterministic)
-        for (size_t i = n; i > 1; --i) {
-            x += 0x9E3779B97F4A7C15ull;
-            unsigned long long z = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-            z ^= z >> 31;
-            std::swap(order[i - 1], order[z % i]);
-        }
+        shuffled(order, seed);
         for (size_t i = 0; i < n; ++i) {
             if (hipMemCreate(&h[i], chunk, &prop, 0) != hipSuccess) {
                 h.resize(i);
@@ -138,6 +131,38 @@ struct VmmBuf {
         }
         return 0;
     }
+    // Map the same physical chunks into the range in the order of another seed
+    // (the placement search of ensure_ws: which chunk backs which part of the
+    // workspace decides how the concurrent streams spread over DRAM channels).
+    int remap(unsigned seed) {
+        if (!va) return fail(TDEC_EINVAL, "remap of an empty VMM buffer");
+        if (hipMemUnmap(va, size) != hipSuccess) return fail(TDEC_EHIP, "hipMemUnmap failed");
+        const size_t n = h.size();
+        std::vector<size_t> order(n);
+        shuffled(order, seed);
+        for (size_t i = 0; i < n; ++i)
+            if (hipMemMap((char *)va + order[i] * chunk, chunk, 0, h[i], 0) != hipSuccess)
+                return fail(TDEC_EHIP, "hipMemMap failed");
+        hipMemAccessDesc acc{};
+        acc.location.type = hipMemLocationTypeDevice;
+        acc.location.id = dev;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        if (hipMemSetAccess(va, size, &acc, 1) != hipSuccess) return fail(TDEC_EHIP, "hipMemSetAccess failed");
+        return 0;
+    }
+    static void shuffled(std::vector<size_t> &order, unsigned seed) {
+        const size_t n = order.size();
+        for (size_t i = 0; i < n; ++i) order[i] = i;
+        unsigned long long x = 0x9E3779B97F4A7C15ull ^ seed;   // splitmix shuffle (deterministic)
+        for (size_t i = n; i > 1; --i) {
+            x += 0x9E3779B97F4A7C15ull;
+            unsigned long long z = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            std::swap(order[i - 1], order[z % i]);
+        }
+    }
+    int dev = 0;
     void release() {
         if (va && size) hipMemUnmap(va, size);
         for (auto &x : h) hipMemRelease(x);
@@ -840,6 +865,9 @@ static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size
 // Opt-in since round 3 (TDEC_PLACEMENT_PROBE=1; bench.py sets it): by default
 // reserve() allocates only its own workspace.
 constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 16;
+#ifndef TDEC_VMM_ORDERS_DEFAULT
+#define TDEC_VMM_ORDERS_DEFAULT 1
+#endif
 constexpr float FAST_VS_MEDIAN = 0.97f;
 
 static int ensure_ws(tdec_t *h, int waves) {
@@ -880,6 +908,37 @@ static int ensure_ws(tdec_t *h, int waves) {
             }
             h->ws.p = h->ws_vmm.va;   // not owned by ws (released through ws_vmm)
             h->ws.cap = total;
+            // TDEC_VMM_ORDERS = K > 1: time a one-iteration decode on K chunk orders of
+            // the same physical chunks (remap) and keep the fastest (a full-size
+            // workspace only)
+            const char *ko = getenv("TDEC_VMM_ORDERS");
+            const int K = std::max(1, std::min(32, ko ? atoi(ko) : TDEC_VMM_ORDERS_DEFAULT));
+            if (K > 1 && waves == h->max_waves) {
+                void *planes = nullptr, *bits = nullptr;
+                hipEvent_t e0 = nullptr, e1 = nullptr;
+                const size_t pb = tdec_planes_bytes(h, waves * WAVE), bb = (size_t)waves * WAVE * 2 * h->N * sizeof(int32_t);
+                const bool ok = hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
+                                hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+                                hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) ==
+                                    hipSuccess;
+                float ms[32];
+                int best = 0;
+                for (int k = 0; ok && k < K; ++k) {
+                    if (k > 0 && h->ws_vmm.remap(12345u + (unsigned)k)) break;
+                    HIPCHK(hipMemsetAsync((char *)h->ws.p + aux_off, 0, WAVE * sizeof(double2), h->stream));
+                    ms[k] = probe_decode_ms(h, waves, (char *)h->ws.p, ck_off, aux_off, (const float *)planes,
+                                            (int32_t *)bits, e0, e1);
+                    if (ms[k] < ms[best]) best = k;
+                    if (getenv("TDEC_PROBE_VERBOSE")) fprintf(stderr, "[tdec] vmm order %d: %.3f ms\n", k, ms[k]);
+                }
+                hipGetLastError();
+                if (e0) hipEventDestroy(e0);
+                if (e1) hipEventDestroy(e1);
+                if (planes) hipFree(planes);
+                if (bits) hipFree(bits);
+                if (ok)
+                    if (int rc = h->ws_vmm.remap(12345u + (unsigned)best)) return rc;
+            }
             h->le_p = (double2 *)h->ws.p;
             h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
             h->aux_p = (double2 *)((char *)h->ws.p + aux_off);

@@ -2271,7 +2271,10 @@ __device__ __forceinline__ double sqrt_1_2_64(double x) {   // sqrt(x) for x in 
 // division by the noise variance, the +-30 clip and the caller's sign.
 // PRE: the caller has checked nv_fast and that |diff| lies in the unscaled range
 // (sym_llrs_pairs16), so the unscaled division runs without a per-LLR test.
-template <typename T, bool FAST = false, bool PRE = false>
+// F32OUT (PRE only): the caller keeps the LLR as f32 (the plane kernels), so the
+// f64 quotient is rounded first and clipped / negated in f32: the same value, since
+// +-30 are f32 values, rounding is monotone and the quotient is finite here.
+template <typename T, bool FAST = false, bool PRE = false, bool F32OUT = false>
 __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
     if constexpr (PRE) {
         if (sizeof(T) == 4 && c.div_f32) {
@@ -2279,6 +2282,10 @@ __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
             float q = div_nr32((float)diff, fn, rcp_nr32(fn));
             q = q < -30.0f ? -30.0f : (q > 30.0f ? 30.0f : q);   // finite: no NaN test
             return (double)(c.sign < 0 ? -q : q);
+        }
+        if constexpr (F32OUT) {
+            const float f = __builtin_amdgcn_fmed3f((float)div_nr64((double)diff, c.nv, rcp_nr64(c.nv)), -30.0f, 30.0f);
+            return (double)(c.sign < 0 ? -f : f);
         }
         double v = div_nr64((double)diff, c.nv, rcp_nr64(c.nv));
         v = v < -30.0 ? -30.0 : (v > 30.0 ? 30.0 : v);
@@ -2377,7 +2384,7 @@ template <typename T, bool FAST = false, bool PRE = false> __device__ __forceinl
 // every candidate's larger |difference| lies between the axes' nearest
 // differences and the largest difference, and every LLR numerator below twice
 // its square; a symbol outside declines (its LLRs come from the full chain).
-template <typename T>
+template <typename T, bool F32OUT = false>
 __device__ __forceinline__ bool sym_llrs_pairs16(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[4]) {
     constexpr bool F32 = sizeof(T) == 4;
     if (!(isfinite(sr) && isfinite(si))) return false;
@@ -2443,18 +2450,18 @@ __device__ __forceinline__ bool sym_llrs_pairs16(T sr, T si, const T *cons, cons
         }
     if (!(fmin(fmin(fabs(diff[0]), fabs(diff[1])), fmin(fabs(diff[2]), fabs(diff[3]))) >= lo)) return false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = llr_from_diff<T, true, true>(diff[k], c);
+    for (int k = 0; k < 4; ++k) out[k] = llr_from_diff<T, true, true, F32OUT>(diff[k], c);
     return true;
 }
 
-template <typename T, int BPS>
+template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr int K = BPS / 2, L = 1 << K;
     const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
     if constexpr (K == 2 && TDEC_DM_PAIRS && dm_fast(BPS)) {
-        if (c.nv_fast) return sym_llrs_pairs16<T>(sr, si, cons, c, out);
+        if (c.nv_fast) return sym_llrs_pairs16<T, F32OUT>(sr, si, cons, c, out);
     }
     T all1[2], all2[2], b1[2][K][2], b2[2][K][2];   // nearest / second nearest: axis, bit-halves
     int arg[2][K][2], allarg[2];
@@ -2574,7 +2581,13 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
 #ifndef TDEC_DM_SCANPRE
 #define TDEC_DM_SCANPRE 1
 #endif
-template <typename T, int BPS, int M = (1 << BPS)>
+// TDEC_DM_F32OUT: the plane kernels take the LLRs' f32 form (llr_from_diff F32OUT):
+// same planes, 16QAM 12.62 -> 12.29 ms, 256QAM 12.82 -> 12.30, 8PSK 11.27 -> 11.11 per
+// 1 M codewords (profiles/r05/demap_f32out/)
+#ifndef TDEC_DM_F32OUT
+#define TDEC_DM_F32OUT 1
+#endif
+template <typename T, int BPS, bool F32OUT = false, int M = (1 << BPS)>
 __device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr bool F32 = sizeof(T) == 4;
     T dx[M], dy[M], lmin = (T)INFINITY, lmax = (T)0;
@@ -2607,7 +2620,7 @@ __device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, con
 #pragma unroll
     for (int b = 0; b < BPS; ++b) {
         const T d = m0[b] - m1[b];
-        if (fabs(d) >= lo) out[b] = llr_from_diff<T, true, true>(d, c);
+        if (fabs(d) >= lo) out[b] = llr_from_diff<T, true, true, F32OUT>(d, c);
         else out[b] = llr_from_diff<T, false>(d, c);
     }
     return true;
@@ -2616,12 +2629,12 @@ __device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, con
 // With every lane's symbol finite (the table is), every difference is finite
 // and |z| is cabs_fin; BPSK / QPSK / 8PSK (M <= 8, the scan is their only
 // path) take that copy when the whole wave qualifies.
-template <typename T, int BPS, int M = (1 << BPS)>
+template <typename T, int BPS, bool F32OUT = false, int M = (1 << BPS)>
 __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     if constexpr (M <= 8) {
         if (__all(isfinite(sr) && isfinite(si))) {
             if constexpr (TDEC_DM_SCANPRE && dm_fast(BPS)) {
-                if (sym_llrs_scan_pre<T, BPS>(sr, si, cons, c, out)) return;
+                if (sym_llrs_scan_pre<T, BPS, F32OUT>(sr, si, cons, c, out)) return;
             }
             sym_llrs_scan<T, BPS, true>(sr, si, cons, c, out);
             return;
@@ -2726,7 +2739,7 @@ __device__ __forceinline__ int gray_inv(int q, int K) {
     for (int sh = 1; sh < K; ++sh) a ^= q >> sh;
     return a;
 }
-template <typename T, int BPS>
+template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr int K = BPS / 2, L = 1 << K;
     if (!(isfinite(sr) && isfinite(si))) return false;
@@ -2795,7 +2808,7 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
             }
             if (!(dlo >= lo)) return false;
 #pragma unroll
-            for (int k = 0; k < BPS; ++k) out[k] = llr_from_diff<T, true, true>(diff[k], c);
+            for (int k = 0; k < BPS; ++k) out[k] = llr_from_diff<T, true, true, F32OUT>(diff[k], c);
             return true;
         }
     }
@@ -2833,7 +2846,7 @@ __device__ __forceinline__ void dm_count(int path, int sep) {
 #else
 __device__ __forceinline__ void dm_count(int, int) {}
 #endif
-template <typename T, int BPS>
+template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
 #ifndef TDEC_DM_GRAY
 #define TDEC_DM_GRAY 1
@@ -2841,14 +2854,14 @@ __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const Demap
     // 64 / 256QAM (measured, 1 M codewords, same planes: 20.2 -> 17.6 ms, 70.3 -> 56.2 ms);
     // 16QAM's 4-level scan is cheaper than the table lookups (14.9 vs 16.0 ms)
     if constexpr (TDEC_DM_GRAY && BPS >= 6 && BPS % 2 == 0) {
-        if (c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out)) return dm_count(1, c.sep);
+        if (c.sep == 2 && sym_llrs_gray<T, BPS, F32OUT>(sr, si, cons, c, out)) return dm_count(1, c.sep);
     }
     if constexpr (BPS >= 8 && BPS % 2 == 0) {
         if (c.sep && sym_llrs_sep_seq<T, BPS>(sr, si, cons, c, out)) return dm_count(2, c.sep);
     } else if constexpr (BPS >= 4 && BPS % 2 == 0) {
-        if (c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out)) return dm_count(2, c.sep);
+        if (c.sep && sym_llrs_sep<T, BPS, F32OUT>(sr, si, cons, c, out)) return dm_count(2, c.sep);
     }
-    sym_llrs<T, BPS>(sr, si, cons, c, out);
+    sym_llrs<T, BPS, F32OUT>(sr, si, cons, c, out);
     dm_count(3, c.sep);
 }
 
@@ -3030,10 +3043,10 @@ struct DemapDecl {
 };
 
 // the fast exact search of a split table; false: declined
-template <typename T, int BPS>
+template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
-    if constexpr (TDEC_DM_GRAY && BPS >= 6) return c.sep == 2 && sym_llrs_gray<T, BPS>(sr, si, cons, c, out);
-    else return c.sep && sym_llrs_sep<T, BPS>(sr, si, cons, c, out);
+    if constexpr (TDEC_DM_GRAY && BPS >= 6) return c.sep == 2 && sym_llrs_gray<T, BPS, F32OUT>(sr, si, cons, c, out);
+    else return c.sep && sym_llrs_sep<T, BPS, F32OUT>(sr, si, cons, c, out);
 }
 
 template <typename T, int BPS, bool SPLIT = false>
@@ -3086,7 +3099,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             double v[BPS];
             if constexpr (SPLIT) {
                 bool dec = false;
-                if (live) dec = !demap_fast<T, BPS>((T)zc.x, (T)zc.y, cons, c, v);
+                if (live) dec = !demap_fast<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
                 // declined symbols go to the list for k_demap_fix (which rewrites their
                 // plane entries): one atomic per wave, entries by lane rank
                 const unsigned long long m = __ballot(dec);
@@ -3105,7 +3118,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                 if (!live || dec) continue;
             } else {
                 if (!live) continue;
-                demap_sym<T, BPS>((T)zc.x, (T)zc.y, cons, c, v);
+                demap_sym<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
             }
 #pragma unroll
             for (int b = 0; b < BPS; ++b) {
@@ -3143,7 +3156,7 @@ __device__ __forceinline__ void dm_fix_symbol(long cw, long s, int N, int S, con
                                               const DemapCfg &c, const int *dst, long n_avail, float *planes) {
     const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
     double v[BPS];
-    demap_sym<T, BPS>((T)z.x, (T)z.y, cons, c, v);
+    demap_sym<T, BPS, TDEC_DM_F32OUT>((T)z.x, (T)z.y, cons, c, v);
     float *base = planes + (cw / WAVE) * tile_floats(N);
     const int lane = (int)(cw & (WAVE - 1));
 #pragma unroll
@@ -3228,7 +3241,7 @@ template <typename T, int BPS> struct DemapPro {
                 if (cw >= B || sy >= S) continue;
                 const float2 z = *reinterpret_cast<const float2 *>(a.syms + 2 * (cw * S + sy));
                 double v[BPS];
-                demap_sym<T, BPS>((T)z.x, (T)z.y, cons, a.c, v);
+                demap_sym<T, BPS, TDEC_DM_F32OUT>((T)z.x, (T)z.y, cons, a.c, v);
 #pragma unroll
                 for (int b = 0; b < BPS; ++b) {
                     const long j = sy * BPS + b;

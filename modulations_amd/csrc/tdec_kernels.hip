@@ -3020,6 +3020,17 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_KC_QPSK
 #define TDEC_DM_KC_QPSK 12
 #endif
+// TDEC_DM_EXP (timing builds only, WRONG PLANES): 1 = phase 1 without the demap
+// arithmetic, to split the kernel's time into its search / LLR work and the rest
+#ifndef TDEC_DM_EXP
+#define TDEC_DM_EXP 0
+#endif
+#ifndef TDEC_DM_PLANAR
+#define TDEC_DM_PLANAR 0
+#endif
+#ifndef TDEC_DM_NOVMW
+#define TDEC_DM_NOVMW 0
+#endif
 constexpr int DM_KC = TDEC_DM_KC;          // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
 constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
@@ -3055,7 +3066,10 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                                                        const int *__restrict__ off, long n_avail, float *planes,
                                                        long n_items, DemapDecl dd) {
     __shared__ T cons[DM_TAB];
-    constexpr int KC = dm_kc(BPS), LD = 6 * KC + 1;   // couples per item, LDS row stride (odd)
+    // couples per item, LDS row stride (odd); TDEC_DM_PLANAR: the tile by label bit
+    // (column b * ns + symbol: the 64 lanes of a phase-1 store hit 64 banks) with room
+    // for the item's straddling symbols
+    constexpr int KC = dm_kc(BPS), LD = TDEC_DM_PLANAR ? 6 * KC + 2 * BPS + 1 : 6 * KC + 1;
     __shared__ float L[WAVE * LD];
     static_assert(!SPLIT || dm_split(BPS), "split only for square 16 / 64 / 256QAM");
     load_table<T, BPS>(cons, cons_g, c);
@@ -3099,7 +3113,10 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             double v[BPS];
             if constexpr (SPLIT) {
                 bool dec = false;
-                if (live) dec = !demap_fast<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
+                if constexpr (TDEC_DM_EXP & 1) {   // timing only: no demap (the loaded symbol, written as LLRs)
+#pragma unroll
+                    for (int b = 0; b < BPS; ++b) v[b] = (double)(b & 1 ? zc.y : zc.x);
+                } else if (live) dec = !demap_fast<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
                 // declined symbols go to the list for k_demap_fix (which rewrites their
                 // plane entries): one atomic per wave, entries by lane rank
                 const unsigned long long m = __ballot(dec);
@@ -3123,7 +3140,8 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
 #pragma unroll
             for (int b = 0; b < BPS; ++b) {
                 const long j = s * BPS + b;
-                if (j >= j0 && j < j1) L[ln * LD + (int)(j - j0)] = (float)v[b];
+                if constexpr (TDEC_DM_PLANAR) L[ln * LD + b * ns + sx] = (float)v[b];
+                else if (j >= j0 && j < j1) L[ln * LD + (int)(j - j0)] = (float)v[b];
             }
         }
         __syncthreads();
@@ -3139,12 +3157,16 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
             for (int cc = 0; cc < 4; ++cc) {
                 if (cc >= nc) break;
                 const int j = src[(long)(half ? 6 + cc : cc) * N + k];
-                v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + (int)(j - j0)] : 0.0f;
+                const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
+                v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
             }
             if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
             else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
         }
-        __syncthreads();   // L is rewritten by the next item
+        // L is rewritten by the next item: its reads done everywhere (TDEC_DM_NOVMW: the
+        // plane stores keep draining behind the next item's phase 1)
+        if constexpr (TDEC_DM_NOVMW) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else __syncthreads();
     }
 }
 

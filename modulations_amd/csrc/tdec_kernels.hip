@@ -3008,8 +3008,8 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_PF
 #define TDEC_DM_PF 1
 #endif
-// TDEC_DM_KC: couples per block (its LDS tile [64][6 * KC + 1] f32 bounds the
-// blocks per CU: 16 -> 27.9 KB, five)
+// TDEC_DM_KC: couples per block (its LDS tile [64][6 * KC + 2 * BPS + 1] f32 bounds
+// the blocks per CU: 16 -> 27-29 KB, five)
 #ifndef TDEC_DM_KC
 #define TDEC_DM_KC 16
 #endif
@@ -3025,9 +3025,14 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_EXP
 #define TDEC_DM_EXP 0
 #endif
+// TDEC_DM_PLANAR: the LDS tile by label bit (column b * ns + symbol), so the 64
+// lanes of a phase-1 store hit 64 banks: 1.5-4 % faster on every table, both A/B
+// orders (16QAM 12.08 vs 12.39 ms, QPSK 5.19 vs 5.37, profiles/r05/demap_planar/)
 #ifndef TDEC_DM_PLANAR
-#define TDEC_DM_PLANAR 0
+#define TDEC_DM_PLANAR 1
 #endif
+// TDEC_DM_NOVMW (with TDEC_DM_PERSIST): the end-of-item barrier does not wait for
+// the plane stores -- measured slower (16QAM 15.1 vs 13.4 ms, profiles/r05/demap_planar/)
 #ifndef TDEC_DM_NOVMW
 #define TDEC_DM_NOVMW 0
 #endif

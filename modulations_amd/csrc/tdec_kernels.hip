@@ -3031,6 +3031,14 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 #ifndef TDEC_DM_PLANAR
 #define TDEC_DM_PLANAR 1
 #endif
+// TDEC_DM_WAVE: each wave of a block owns 16 of the tile's 64 codewords, both
+// phases -- its LDS rows are its own, so the phases meet at no block barrier and
+// the waves of a CU drift apart (one wave's plane stores drain behind another's
+// search); phase 2 stores 4 x 256 B per instruction.  Measured slower on every
+// table (16QAM 13.95 vs 12.63 ms, QPSK 5.9-6.1 vs 5.37, profiles/r05/demap_wave/)
+#ifndef TDEC_DM_WAVE
+#define TDEC_DM_WAVE 0
+#endif
 // TDEC_DM_NOVMW (with TDEC_DM_PERSIST): the end-of-item barrier does not wait for
 // the plane stores -- measured slower (16QAM 15.1 vs 13.4 ms, profiles/r05/demap_planar/)
 #ifndef TDEC_DM_NOVMW
@@ -3077,6 +3085,9 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
     constexpr int KC = dm_kc(BPS), LD = TDEC_DM_PLANAR ? 6 * KC + 2 * BPS + 1 : 6 * KC + 1;
     __shared__ float L[WAVE * LD];
     static_assert(!SPLIT || dm_split(BPS), "split only for square 16 / 64 / 256QAM");
+    constexpr bool WV = TDEC_DM_WAVE != 0;
+    constexpr int CPW = WAVE / (BLOCK / WAVE);   // TDEC_DM_WAVE: codewords per wave
+    const int wv = (int)threadIdx.x / WAVE, me = (int)threadIdx.x & (WAVE - 1);
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + KC - 1) / KC;
     __syncthreads();
@@ -3088,10 +3099,13 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
         const int ns = (int)(s1 - s0);
         // item t = (lane, si), consecutive threads: consecutive symbols; the
-        // quotient and remainder of t by ns advance by those of BLOCK each step
-        const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
-        int lane = (int)threadIdx.x / ns, si = (int)threadIdx.x - lane * ns;
-        const int nt = WAVE * ns;
+        // quotient and remainder of t by ns advance by those of STEP each step
+        // (TDEC_DM_WAVE: t over the wave's own codewords, lanes LN0 + ...)
+        constexpr int STEP = WV ? WAVE : BLOCK, NL = WV ? CPW : WAVE;
+        const int T0 = WV ? me : (int)threadIdx.x, LN0 = WV ? wv * CPW : 0;
+        const int dq = STEP / ns, dr = STEP - dq * ns;
+        int lane = T0 / ns, si = T0 - lane * ns;
+        const int nt = NL * ns;
         // the symbol of item t (lane ln, symbol sx), zero past the batch / the item's end
         auto sym_at = [&](int t, int ln, int sx) -> float2 {
             const long cw = tile * WAVE + ln, s = s0 + sx;
@@ -3101,9 +3115,9 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
         // TDEC_DM_PF: the next item's symbol is loaded before this one is demapped
         // (8PSK / 16QAM: measured faster; QPSK and 64 / 256QAM slower)
         constexpr bool PF = TDEC_DM_PF && (BPS == 3 || BPS == 4);
-        float2 zn = PF ? sym_at((int)threadIdx.x, lane, si) : make_float2(0.0f, 0.0f);
-        for (int t = threadIdx.x; t < nt; t += BLOCK) {
-            const int ln = lane, sx = si;
+        float2 zn = PF ? sym_at(T0, LN0 + lane, si) : make_float2(0.0f, 0.0f);
+        for (int t = T0; t < nt; t += STEP) {
+            const int ln = LN0 + lane, sx = si;
             lane += dq;
             si += dr;
             if (si >= ns) {
@@ -3111,7 +3125,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                 ++lane;
             }
             const float2 zc = PF ? zn : sym_at(t, ln, sx);
-            if (PF) zn = sym_at(t + BLOCK, lane, si);
+            if (PF) zn = sym_at(t + STEP, LN0 + lane, si);
             const long cw = tile * WAVE + ln;
             const long s = s0 + sx;
             const bool live = cw < B && s < S;
@@ -3126,7 +3140,7 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                 // plane entries): one atomic per wave, entries by lane rank
                 const unsigned long long m = __ballot(dec);
                 if (m) {
-                    const int leader = __ffsll((long long)m) - 1, me = threadIdx.x & (WAVE - 1);
+                    const int leader = __ffsll((long long)m) - 1;
                     unsigned base = 0;
                     if (me == leader) base = atomicAdd(dd.count, (unsigned)__popcll(m));
                     base = __shfl(base, leader);
@@ -3149,8 +3163,40 @@ __global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, con
                 else if (j >= j0 && j < j1) L[ln * LD + (int)(j - j0)] = (float)v[b];
             }
         }
-        __syncthreads();
         float *base = planes + tile * tile_floats(N);
+        if constexpr (WV) {
+            // the wave reads back only rows its own lanes wrote: LDS operations of one
+            // wave complete in order, so a compiler barrier is all the ordering needed
+            asm volatile("" ::: "memory");
+            const int nk = k1 - k0;
+            for (int t = me; t < CPW * nk; t += WAVE) {   // float4 entries: 16 lanes x 4 steps
+                const int k = k0 + t / CPW, lane = LN0 + (t & (CPW - 1));
+                const long cw = tile * WAVE + lane;
+                float v[4];
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int j = src[(long)cc * N + k];
+                    const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
+                    v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
+                }
+                reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            for (int t = me; t < CPW * nk; t += WAVE) {   // float2 entries
+                const int k = k0 + t / CPW, lane = LN0 + (t & (CPW - 1));
+                const long cw = tile * WAVE + lane;
+                float v[2];
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc) {
+                    const int j = src[(long)(6 + cc) * N + k];
+                    const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
+                    v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
+                }
+                reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
+            }
+            asm volatile("" ::: "memory");
+            continue;
+        }
+        __syncthreads();
         for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
             const int lane = t & (WAVE - 1);
             const int q = __builtin_amdgcn_readfirstlane(t >> 6);   // (step, half): wave-uniform, so src[] is read by scalar loads

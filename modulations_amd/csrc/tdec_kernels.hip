@@ -3073,8 +3073,21 @@ __device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const Dema
     else return c.sep && sym_llrs_sep<T, BPS, F32OUT>(sr, si, cons, c, out);
 }
 
+// TDEC_DM_WPE: the plane kernels' minimum waves per SIMD (amdgpu_waves_per_eu: the
+// register budget 512 / WPE; 0 = the compiler's choice).  The f64 split kernels hold
+// 133 / 141 / 169 VGPRs (16 / 64 / 256QAM: 3, 3, 2 waves per SIMD); 4 or 3 waves
+// measured the same (16QAM 12.10 vs 12.10-12.16 ms, profiles/r05/demap_wpe/): the
+// kernel is not latency-bound, so its f64 instruction count is what sets its time
+#ifndef TDEC_DM_WPE
+#define TDEC_DM_WPE 0
+#endif
+#if TDEC_DM_WPE > 0
+#define TDEC_DM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TDEC_DM_WPE)))
+#else
+#define TDEC_DM_WPE_ATTR
+#endif
 template <typename T, int BPS, bool SPLIT = false>
-__global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
+__global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *__restrict__ src,
                                                        const int *__restrict__ off, long n_avail, float *planes,
                                                        long n_items, DemapDecl dd) {

@@ -4,8 +4,8 @@ declines; k_demap_fix gives those the full chain and rewrites their plane
 entries, and redoes every symbol of a tile whose declines overflowed the list.
 
 Checked against the host chain the reference runs (compute_llr,
-test_sdr_with_coding.py:200-225, decoder sign, truncated / zero-padded to
-n_coded, :474-478), put into the same tile planes by the depuncture kernel:
+test_sdr_with_coding.py:200-225, decoder sign, truncated / zero-padded as
+:474-478 to the decoder's LLR count), put into the same tile planes by the depuncture kernel:
 the planes must be equal (NaN == NaN), on symbols that are declined often
 (ties, near-ties, NaN / inf, out-of-grid) and on a batch whose declines
 overflow the list (most symbols NaN)."""
@@ -62,8 +62,14 @@ def _check(c, syms, mod, nv, cons=None):
     fin = ~np.isnan(flat)
     llr.reshape(-1, bps)[fin] = (-O.demap(flat[fin], cons, bps, nve, div_f32=div32)).reshape(-1, bps)
     llr = llr.reshape(B, -1)
-    ref_llr = np.zeros((B, c.n_coded), np.float32)
-    m = min(c.n_coded, llr.shape[1])
+    # zero-padded / truncated to the decoder's LLR count, the de-puncture walk
+    # (include/tdec.h, tdec_demap_planes_dev).  It equals the reference's n_coded
+    # when the puncture period divides N; otherwise (N = 212 / 752 at rate 2/3)
+    # n_coded is shorter than the walk and the reference's chain raises IndexError
+    # in decode() (test_sdr_with_coding.py:474-480, dvb_rcs2_turbo.py:476-487)
+    L = c.handle.llr_len
+    ref_llr = np.zeros((B, L), np.float32)
+    m = min(L, llr.shape[1])
     ref_llr[:, :m] = llr[:, :m]
     ref = torch.empty_like(planes)
     c.depuncture_device(torch.from_numpy(ref_llr).cuda(), ref)
@@ -72,9 +78,24 @@ def _check(c, syms, mod, nv, cons=None):
 
 
 @pytest.mark.parametrize("mod,n,rate", [("16QAM", 752, "1/3"), ("64QAM", 212, "1/2"), ("256QAM", 752, "1/3"),
-                                        ("256QAM", 48, "3/4")])
+                                        ("256QAM", 48, "3/4"), ("16QAM", 212, "2/3"), ("64QAM", 752, "2/3")])
 def test_split_planes_equal_host_chain(mod, n, rate):
     rng = np.random.default_rng(sum(map(ord, mod)) + n)
+    c = M.DVBRCS2_Turbo(n, rate)
+    bps = D.MODULATIONS[mod]["bps"]
+    S = -(-c.n_coded // bps)
+    _check(c, _adversarial(D.constellation(mod), rng, (130, S)), mod, 0.04)
+
+
+@pytest.mark.parametrize("mod,n,rate", [("BPSK", 752, "1/3"), ("BPSK", 48, "3/4"), ("QPSK", 212, "1/3"),
+                                        ("QPSK", 752, "2/3"), ("8PSK", 752, "1/2"), ("8PSK", 752, "3/4"),
+                                        ("8PSK", 64, "2/3")])
+def test_inline_planes_equal_host_chain(mod, n, rate):
+    """The tables demapped inline (no split) through the same plane kernel and its
+    planar LDS tile (column b * ns + symbol): BPSK's 96-symbol items (more
+    symbols than lanes), 8PSK's straddling symbols at 3/4 (2068 LLRs, 3 per
+    symbol), a ragged last tile (130 codewords), adversarial symbols."""
+    rng = np.random.default_rng(sum(map(ord, mod)) + n + len(rate))
     c = M.DVBRCS2_Turbo(n, rate)
     bps = D.MODULATIONS[mod]["bps"]
     S = -(-c.n_coded // bps)
@@ -119,8 +140,14 @@ def test_tables_the_fast_search_cannot_take_stay_inline(kind):
     planes = torch.empty(c.planes_bytes(B) // 4, dtype=torch.float32, device="cuda")
     c.demap_planes_device(torch.from_numpy(syms).cuda(), cons, bps, nve, planes, div_f32=div32)
     llr = np.stack([-O.demap(r, cons, bps, nve, div_f32=div32) for r in syms])
-    ref_llr = np.zeros((B, c.n_coded), np.float32)
-    m = min(c.n_coded, llr.shape[1])
+    # zero-padded / truncated to the decoder's LLR count, the de-puncture walk
+    # (include/tdec.h, tdec_demap_planes_dev).  It equals the reference's n_coded
+    # when the puncture period divides N; otherwise (N = 212 / 752 at rate 2/3)
+    # n_coded is shorter than the walk and the reference's chain raises IndexError
+    # in decode() (test_sdr_with_coding.py:474-480, dvb_rcs2_turbo.py:476-487)
+    L = c.handle.llr_len
+    ref_llr = np.zeros((B, L), np.float32)
+    m = min(L, llr.shape[1])
     ref_llr[:, :m] = llr[:, :m]
     ref = torch.empty_like(planes)
     c.depuncture_device(torch.from_numpy(ref_llr).cuda(), ref)

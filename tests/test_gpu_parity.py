@@ -193,6 +193,9 @@ def test_decode_iterations_and_errors():
     with pytest.raises(IndexError):
         c.decode(np.zeros(c.n_coded - 1))            # the reference's de-puncture IndexError
     assert c.decode(np.zeros(c.n_coded + 5)).shape == (96,)   # extra LLRs are ignored
+    c = M.DVBRCS2_Turbo(212, "2/3")   # period 3 does not divide N: n_coded (630) < the walk (636)
+    with pytest.raises(IndexError):
+        c.decode(np.zeros(c.n_coded))                # what the reference's receive chain hands decode()
     with pytest.raises(UnboundLocalError):
         M.DVBRCS2_Turbo(48, "1/3", iterations=0).decode(np.zeros(288))
     bad = list(_tabs())

@@ -40,7 +40,8 @@ def _two_launch(codec, mod, syms, n0, lfinal=False):
                                               ("256QAM", 752, "1/3", "max-log", 1000),
                                               ("QPSK", 212, "1/3", "max-log", 777),
                                               ("8PSK", 752, "1/2", "log-map", 300),
-                                              ("16QAM", 48, "1/2", "max-log", 65)])
+                                              ("16QAM", 48, "1/2", "max-log", 65),
+                                              ("16QAM", 212, "2/3", "max-log", 130)])
 def test_fused_equals_two_launch_path(mod, n, rate, algo, B):
     codec = M.DVBRCS2_Turbo(n, rate, algo=algo)
     cons = D.constellation(mod)

@@ -3074,10 +3074,10 @@ __device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const Dema
 }
 
 // TDEC_DM_WPE: the plane kernels' minimum waves per SIMD (amdgpu_waves_per_eu: the
-// register budget 512 / WPE; 0 = the compiler's choice).  The f64 split kernels hold
-// 133 / 141 / 169 VGPRs (16 / 64 / 256QAM: 3, 3, 2 waves per SIMD); 4 or 3 waves
-// measured the same (16QAM 12.10 vs 12.10-12.16 ms, profiles/r05/demap_wpe/): the
-// kernel is not latency-bound, so its f64 instruction count is what sets its time
+// register budget 512 / WPE; 0 = the compiler's choice).  It binds only the f64
+// instances (complex128 tables: 133 / 141 / 169 VGPRs for 16 / 64 / 256QAM); the
+// complex64 tables the bench times hold 85 / 77 / 89 and are unchanged by it, so
+// the A/B in profiles/r05/demap_wpe/ (same times) measured nothing about them
 #ifndef TDEC_DM_WPE
 #define TDEC_DM_WPE 0
 #endif

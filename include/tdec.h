@@ -87,6 +87,10 @@ int tdec_siso_batch_f64(tdec_t *h, int B, const double *LcA, const double *LcB, 
  * tdec_siso_staging call asks for more rows, or tdec_destroy. */
 int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes);
 int tdec_siso_staged(tdec_t *h, int B, int lc_f64, double sf);
+/* Staged calls that waited for their rows' completion flags longer than the
+ * library's time limit and ended by a stream synchronisation instead (a
+ * diagnostic: the flags live in coherent host memory, so this stays 0). */
+int tdec_siso_stats(const tdec_t *h, long *flag_fallbacks);
 
 /* Full turbo decode of B codewords: replaces DVBRCS2_Turbo.decode
  * (dvb_rcs2_turbo.py:464-537; historic name turbo_decode).  llr rows of

@@ -30,7 +30,7 @@ EXPORTS = (
     "tdec_demap_batch", "tdec_constellation", "tdec_workload_dev", "tdec_info_bits_dev", "tdec_count_errors_dev",
     "tdec_reserve_fused", "tdec_fused_available", "tdec_demap_decode_dev", "tdec_selftest", "tdec_selftest_trans",
     "tdec_host_alloc", "tdec_host_free", "tdec_encode_host", "tdec_siso_batch_f64", "tdec_siso_staging",
-    "tdec_siso_staged",
+    "tdec_siso_staged", "tdec_siso_stats",
 )
 
 _lib = None
@@ -58,6 +58,9 @@ def _declare(L):
         L.tdec_siso_staging.restype = C.c_int
         L.tdec_siso_staged.argtypes = [_vp, C.c_int, C.c_int, C.c_double]
         L.tdec_siso_staged.restype = C.c_int
+    if hasattr(L, "tdec_siso_stats"):
+        L.tdec_siso_stats.argtypes = [_vp, C.POINTER(C.c_long)]
+        L.tdec_siso_stats.restype = C.c_int
     L.tdec_decode_batch.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
     L.tdec_reserve.argtypes = [_vp, C.c_int]
     L.tdec_planes_bytes.argtypes = [_vp, C.c_int]
@@ -65,7 +68,8 @@ def _declare(L):
     L.tdec_depuncture_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp]
     L.tdec_decode_planes_dev.argtypes = [_vp, C.c_int, _vp, _vp, _vp, _vp]
     L.tdec_decode_batch_dev.argtypes = [_vp, C.c_int, _vp, C.c_long, _vp, _vp, _vp]
-    L.tdec_tail_gate.argtypes = [_vp, _vp]
+    if hasattr(L, "tdec_tail_gate"):   # (A/B tools also load older builds without it)
+        L.tdec_tail_gate.argtypes = [_vp, _vp]
     L.tdec_demap_dev.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,
                                  C.c_int, C.c_int, _vp, _vp]
     L.tdec_demap.argtypes = [C.c_int, _vp, C.c_int, C.c_long, _vp, C.c_int, C.c_int, C.c_int, C.c_double,

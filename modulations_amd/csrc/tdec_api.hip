@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -61,16 +62,18 @@ struct DevBuf {
 
 // Page-locked host staging for the small host-pointer calls (grown on demand).
 // dev: the buffer's device address (zero-copy kernels read / write it directly),
-// looked up once per allocation instead of per call.
+// looked up once per allocation instead of per call.  flags: hipHostMalloc flags
+// (hipHostMallocDefault; the SISO completion flags take coherent, mapped memory,
+// which the host may poll while the kernel that writes it still runs).
 struct PinBuf {
     void *p = nullptr, *dev = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    int ensure(size_t bytes, unsigned flags = hipHostMallocDefault) {
         if (bytes <= cap) return 0;
         if (p) hipHostFree(p);
         p = dev = nullptr;
         cap = 0;
-        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return fail(TDEC_ENOMEM, "hipHostMalloc failed");
+        if (hipHostMalloc(&p, bytes, flags) != hipSuccess) return fail(TDEC_ENOMEM, "hipHostMalloc failed");
         if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) dev = nullptr;
         cap = bytes;
         return 0;
@@ -129,25 +132,6 @@ struct VmmBuf {
             release();
             return fail(TDEC_EHIP, "hipMemSetAccess failed");
         }
-        return 0;
-    }
-    // Map the same physical chunks into the range in the order of another seed
-    // (the placement search of ensure_ws: which chunk backs which part of the
-    // workspace decides how the concurrent streams spread over DRAM channels).
-    int remap(unsigned seed) {
-        if (!va) return fail(TDEC_EINVAL, "remap of an empty VMM buffer");
-        if (hipMemUnmap(va, size) != hipSuccess) return fail(TDEC_EHIP, "hipMemUnmap failed");
-        const size_t n = h.size();
-        std::vector<size_t> order(n);
-        shuffled(order, seed);
-        for (size_t i = 0; i < n; ++i)
-            if (hipMemMap((char *)va + order[i] * chunk, chunk, 0, h[i], 0) != hipSuccess)
-                return fail(TDEC_EHIP, "hipMemMap failed");
-        hipMemAccessDesc acc{};
-        acc.location.type = hipMemLocationTypeDevice;
-        acc.location.id = dev;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        if (hipMemSetAccess(va, size, &acc, 1) != hipSuccess) return fail(TDEC_EHIP, "hipMemSetAccess failed");
         return 0;
     }
     static void shuffled(std::vector<size_t> &order, unsigned seed) {
@@ -368,7 +352,7 @@ struct tdec_ctx {
     int n_cu = 0;                      // compute units of the device
     int32_t *d_perm = nullptr, *d_inv = nullptr, *d_src = nullptr, *d_off = nullptr;
     int32_t *d_dst = nullptr;          // LLR index -> c * N + k of the plane component it feeds (-1: none)
-    // k_demap_planes' decline list (TDEC_DM_SPLIT): entries, count, per-tile overflow flags
+    // k_demap_planes' decline list (split tables): entries, count, per-tile overflow flags
     int2 *d_decl = nullptr;
     unsigned *d_decl_n = nullptr;
     unsigned char *d_decl_ovf = nullptr;
@@ -379,29 +363,28 @@ struct tdec_ctx {
     int n_used = 0;
     int max_couple_llrs = 0;           // most LLRs any couple consumes (<= 6)
     DevBuf ws;                         // per-wave decode workspace: extrinsic planes + checkpoints
-    VmmBuf ws_vmm;                     //   or the same as shuffled physical chunks (TDEC_WS_ALLOC=vmm)
+    VmmBuf ws_vmm;                     //   as shuffled physical chunks (>= 1 GiB)
     double2 *le_p = nullptr;           //   extrinsic planes P1 / Le2 / Le1 (inside ws)
     double2 *aux_p = nullptr;          //   a zero row (64 lanes) + per-wave sink rows (inside ws)
     int *d_tile_ctr = nullptr;         // the decoders' tile queue counter (zeroed before each launch)
     unsigned *d_tail = nullptr;        // the throughput decoder's tail flag (DecodeArgs::tail_flag)
     unsigned tail_seq = 0;             // sequence number of its last whole-tile launch
-    int *d_simd_prog = nullptr;        // TDEC_PRIO 4 builds: per-SIMD progress slots (zeroed before each launch)
+    int *d_simd_prog = nullptr;        // max-log issue priority: per-SIMD progress slots (zeroed before each launch)
     float4 *ck_p = nullptr;            //   alpha checkpoints + beta1 ring (inside ws)
     int ws_waves = 0;
-    int row_pad = 0;   // TDEC_ROW_PAD (placement study): lanes of padding per workspace row
     DevBuf planes_own;                 // planes for tdec_decode_batch(_dev)
     int cap_batch = 0;
     DevBuf h_llr, h_bits, h_lf, h_misc; // staging for the host-pointer API
     PinBuf pin;                        // page-locked staging of the small host-pointer calls
     PinBuf pin_siso;                   // the caller-filled SISO staging (tdec_siso_staging), never regrown behind its views
+    PinBuf pin_flags;                  //   its per-row completion flags (fine-grained: coherent while a kernel runs)
     int siso_rows = 0;                 //   rows it holds
-    unsigned siso_seq = 0;             //   the last call's sequence number in its completion flags (after the 8 slots)
+    unsigned siso_seq = 0;             //   the last call's sequence number in its completion flags
+    long siso_fallbacks = 0;           //   staged calls that ended by a stream wait instead of their flags
     ConsCache cons;                    // demapper constellation
     DevBuf spl_ck;                     // checkpoints of the state-per-lane SISO prototype (TDEC_SISO_SPL=1)
     DevBuf planes_w;                   // per-wave plane buffers of the fused demap + decode
     DevBuf ll_ws, ll_st;               // small-batch decoders: extrinsic planes (frame: Le1 only), alpha / beta stores
-    DevBuf iq_le2, iq_ctl, iq_ring;    // the throughput decoders' item queue (TDEC_ITEMQ): per-tile Le2, control, rings
-    int iq_tiles = 0;                  //   tiles they are sized for
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;     // uploads of the chunked host-pointer path (created on first use)
     hipStream_t dstream = nullptr;     // its downloads (a second copy engine direction)
@@ -551,7 +534,7 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     if (e == hipSuccess) e = hipMalloc(&h->d_tile_ctr, sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&h->d_tail, sizeof(unsigned));
     if (e == hipSuccess) e = hipMemset(h->d_tail, 0, sizeof(unsigned));
-    if (e == hipSuccess && TDEC_PRIO == 4) e = hipMalloc(&h->d_simd_prog, SIMD_PROG_BYTES);
+    if (e == hipSuccess && algo == TDEC_ALGO_MAXLOG) e = hipMalloc(&h->d_simd_prog, SIMD_PROG_BYTES);
     if (e == hipSuccess) e = hipMalloc(&h->d_off, sizeof(int32_t) * (N + 1));
     if (e == hipSuccess) e = hipMemcpy(h->d_off, off.data(), sizeof(int32_t) * (N + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->d_perm, perm, sizeof(int32_t) * N, hipMemcpyHostToDevice);
@@ -570,17 +553,11 @@ int tdec_create(int device, int n_couples, int period, const uint8_t *punct, int
     }
     h->max_waves = std::max(1, blocks_per_cu) * n_cu * DEC_WAVES;
     h->n_cu = n_cu;
-    if (const char *rp = getenv("TDEC_ROW_PAD")) h->row_pad = std::max(0, atoi(rp));
     // the kernels address one workspace plane / the checkpoint array with 32-bit
     // byte offsets: rows of n_waves * 64 lanes must keep them below 4 GiB
     const long row_units = std::max<long>(rows_of(N), 4L * ((N + ck_win_of(algo) - 1) / ck_win_of(algo) + RING));
     const long cap = (long)(4294967295UL / ((unsigned long)row_units * WAVE * 16UL));
     h->max_waves = (int)std::max<long>(1, std::min<long>(h->max_waves, cap));
-    // experiment knob: run the persistent decoder on a percentage of the resident waves
-    if (const char *pw = getenv("TDEC_WAVES_PCT")) {
-        const int pct = std::max(1, std::min(100, atoi(pw)));
-        h->max_waves = std::max(DEC_WAVES, h->max_waves * pct / 100 / DEC_WAVES * DEC_WAVES);
-    }
     *out = h;
     return TDEC_OK;
 }
@@ -627,7 +604,7 @@ void tdec_destroy(tdec_t *h) {
 #endif
 #if TDEC_WAVE_TIMING
     {   // measurement build: wave finish-time spread of the last decode launch
-        static unsigned long long t[WT_MAX][2];
+        static unsigned long long t[WT_MAX][4];
         static int nt[WT_MAX];
         hipDeviceSynchronize();
         const int n = std::min(h->max_waves, WT_MAX);
@@ -648,10 +625,18 @@ void tdec_destroy(tdec_t *h) {
                 if (FILE *f = fopen(dump, "a"); f && hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_wave_hw), sizeof(hw)) == hipSuccess) {
                     fprintf(f, "# launch waves=%d\n", n);
                     for (int i = 0; i < n; ++i)
-                        fprintf(f, "%d %llu %llu %d %u %u\n", i, t[i][0], t[i][1], nt[i], hw[i][0], hw[i][1]);
+                        fprintf(f, "%d %llu %llu %d %u %u %llu %llu\n", i, t[i][0], t[i][1], nt[i], hw[i][0], hw[i][1],
+                                t[i][2], t[i][3]);
                     fclose(f);
                 }
             }
+            // the shader clock each wave ran at: s_memtime ticks over s_memrealtime (100 MHz)
+            double ck_sum = 0, ck_min = 1e30, ck_max = 0;
+            for (int i = 0; i < n; ++i) {
+                const double ghz = (double)(t[i][3] - t[i][2]) / std::max(1.0, (double)(t[i][1] - t[i][0]) * 10.0);
+                ck_sum += ghz, ck_min = std::min(ck_min, ghz), ck_max = std::max(ck_max, ghz);
+            }
+            fprintf(stderr, "[tdec] wave clock: mean %.3f GHz (min %.3f, max %.3f)\n", ck_sum / n, ck_min, ck_max);
             std::sort(end.begin(), end.end());
             const double span = (t1 - t0) * 1e-5;
             fprintf(stderr,
@@ -708,14 +693,12 @@ void tdec_destroy(tdec_t *h) {
     h->h_misc.release();
     h->pin.release();
     h->pin_siso.release();
+    h->pin_flags.release();
     h->cons.buf.release();
     h->spl_ck.release();
     h->planes_w.release();
     h->ll_ws.release();
     h->ll_st.release();
-    h->iq_le2.release();
-    h->iq_ctl.release();
-    h->iq_ring.release();
     if (h->stream) hipStreamDestroy(h->stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->dstream) hipStreamDestroy(h->dstream);
@@ -806,70 +789,31 @@ static int ck_rows_of(const tdec_t *h) { return (h->N + ck_win_of(h->algo) - 1) 
 static long ck_stride_of(const tdec_t *h) { return (long)(ck_rows_of(h) + RING) * 4 * WAVE; }
 
 // The decoders' tile queue: the counter zeroed on the launch's stream, or null
-// (static striding) below 4 tiles per wave or with TDEC_DYN_TILES=0.  Measured
-// (same bits): 1 M codewords (8 tiles per wave) 243.8 -> 241.6 ms; at 2 tiles
-// per wave the queue was no faster (max-log 61.8 vs 62.6, log-MAP 381.2 vs
-// 385.9 ms per 262 144), hence the threshold.
+// (static striding) below 4 tiles per wave.  Measured (same bits): 1 M codewords
+// (8 tiles per wave) 243.8 -> 241.6 ms; at 2 tiles per wave the queue was no
+// faster (max-log 61.8 vs 62.6, log-MAP 381.2 vs 385.9 ms per 262 144), hence the
+// threshold.
 static int *tile_queue(tdec_t *h, int tiles, int waves, hipStream_t st) {
-#ifndef TDEC_DYN_DEFAULT
-#define TDEC_DYN_DEFAULT 1
-#endif
-    static const bool dyn = [] {
-        const char *e = getenv("TDEC_DYN_TILES");
-        return e ? e[0] != '0' : TDEC_DYN_DEFAULT != 0;
-    }();
-    if (!dyn || tiles < 4 * waves) return nullptr;
+    if (tiles < 4 * waves) return nullptr;
     if (hipMemsetAsync(h->d_tile_ctr, 0, sizeof(int), st) != hipSuccess) return nullptr;
     return h->d_tile_ctr;
-}
-
-// Time one single-iteration decode of waves*64 codewords of constant LLRs on a
-// candidate workspace (the placement probe below).
-static float probe_decode_ms(tdec_t *h, int waves, char *ws, size_t ck_off, size_t aux_off, const float *planes,
-                             int32_t *bits,
-                             hipEvent_t e0, hipEvent_t e1) {
-    const int B = waves * WAVE;
-    DecodeArgs a{B, h->N, 1, waves, waves, planes, (double2 *)ws, (float4 *)(ws + ck_off), bits, nullptr, h->d_used,
-                 h->row_pad, (double2 *)(ws + aux_off), nullptr, ck_rows_of(h)};
-    const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
-    const void *k = decode_kernel(h->algo, h->N % win_of(h->algo) != 0);
-    float best = 1e30f;
-    for (int rep = 0; rep < 2; ++rep) {
-        hipEventRecord(e0, h->stream);
-        hipLaunchKernelGGL((decode_fn)k, grid, dim3(DEC_BLOCK), 0, h->stream, a, (const int *)h->d_perm,
-                           (const int *)h->d_inv, (const int *)h->d_used);
-        hipEventRecord(e1, h->stream);
-        if (hipEventSynchronize(e1) != hipSuccess) return 1e30f;
-        float ms = 0.0f;
-        hipEventElapsedTime(&ms, e0, e1);
-        best = std::min(best, ms);
-    }
-    return best;
 }
 
 // Workspace for `waves` concurrently decoding waves: the extrinsic planes and
 // the checkpoints in one allocation (checkpoints on the next 2 MiB boundary).
 //
-// Placement probe.  The decode rate depends on where in HBM this workspace
-// lands: on MI355X a full-size workspace (6.4 GB at N = 752) decodes anywhere
-// from ~70 to ~80 ms per 262 144 codewords depending on the allocation (the
-// first allocations of a process tend to be slow), the planes' placement does
-// not matter (tools/placement.py).  So a full-GPU workspace of
-// >= 1 GiB is allocated PROBE_CANDIDATES times, each candidate times a
-// one-iteration decode of constant LLRs, and the fastest is kept (the others
-// are freed).  The candidate times are bimodal: a fast placement probes >= 3 %
-// below the median of its round; when the best of a round is not (every
-// candidate slow; seen in 1 of 6 fresh processes) another round of candidates
-// is allocated while the first ones are still held, up to MAX_CANDIDATES and
-// half of the free memory.  Setup cost: a few hundred ms, once per reserve.
-// Opt-in since round 3 (TDEC_PLACEMENT_PROBE=1; bench.py sets it): by default
-// reserve() allocates only its own workspace.
-constexpr int PROBE_CANDIDATES = 8, MAX_CANDIDATES = 16;
-#ifndef TDEC_VMM_ORDERS_DEFAULT
-#define TDEC_VMM_ORDERS_DEFAULT 1
-#endif
-constexpr float FAST_VS_MEDIAN = 0.97f;
-
+// Placement.  The decode rate depends on where in HBM this workspace lands: on
+// MI355X a full-size workspace (6.4 GB at N = 752) from one hipMalloc decodes
+// anywhere from ~70 to ~80 ms per 262 144 codewords depending on the physical
+// pages it gets (DRAM read-credit stalls on a slow placement; the
+// planes' placement does not matter).  A workspace of >= 1 GiB is therefore built
+// from 64 MiB physical chunks mapped into one virtual range in a fixed shuffled
+// order (VmmBuf), which places it scattered by construction: measured as fast as
+// the best of a timed 8-16-candidate placement probe in every fresh process, with
+// no transient trial allocations (profiles/r03m/, r03n/vmm_ab.txt; the probe,
+// physically contiguous ranges, row padding, chunk sizes >= 128 MiB and searches
+// over chunk orders are in the DESIGN.md appendix).  Smaller workspaces, or a
+// device without VMM support, take one hipMalloc.
 static int ensure_ws(tdec_t *h, int waves) {
     if (waves <= h->ws_waves) return 0;
     if (h->ws_vmm.va) {   // regrowth of a VMM workspace: drop it first (not a hipMalloc pointer)
@@ -878,138 +822,27 @@ static int ensure_ws(tdec_t *h, int waves) {
         h->ws_vmm.release();
     }
     const size_t MB2 = 2u << 20;
-    // rows of waves*64 lanes (+ row_pad): the planes have 3N rows, the checkpoints ck_stride_of / 64
-    const size_t row = (size_t)waves * WAVE + h->row_pad;
+    // rows of waves*64 lanes: the planes have 3N rows, the checkpoints ck_stride_of / 64
+    const size_t row = (size_t)waves * WAVE;
     const size_t le_bytes = row * (ws_stride_of(h) / WAVE) * sizeof(double2);
     const size_t ck_off = (le_bytes + MB2 - 1) / MB2 * MB2;
     // aux: the all-zero a-priori row of the first iteration (64 lanes, zeroed
     // below) and one sink row per wave for the stores the decoder discards
     const size_t aux_off = ck_off + row * (ck_stride_of(h) / WAVE) * sizeof(float4);
     const size_t total = aux_off + ((size_t)WAVE + row) * sizeof(double2);
-    // The placement probe is opt-in (TDEC_PLACEMENT_PROBE=1): by default a workspace of
-    // >= 1 GiB is built from 64 MiB physical chunks mapped in a shuffled order
-    // (VmmBuf), which places it scattered by construction -- measured as fast as the
-    // probe's best candidate in every fresh process (profiles/r03m/vmm_ab.txt) with
-    // no transient trial allocations.  TDEC_WS_ALLOC=malloc / contiguous are the
-    // measurement alternatives (one hipMalloc / one physically contiguous range).
-    const char *pe = getenv("TDEC_PLACEMENT_PROBE");
-    const bool probe = pe && pe[0] == '1' && waves == h->max_waves && total >= (1ul << 30);
-    if (!probe) {
-        const char *wa = getenv("TDEC_WS_ALLOC");
-        const bool vmm = wa ? !strcmp(wa, "vmm") : total >= (1ul << 30);
-        if (vmm) {
-            h->ws.release();
-            const char *cm = getenv("TDEC_VMM_CHUNK_MB");
-            const size_t chunk = (size_t)std::max(1, cm ? atoi(cm) : 64) << 20;
-            if (h->ws_vmm.alloc(h->device, total, chunk, 12345u)) {   // no VMM support: one hipMalloc
-                hipGetLastError();
-                if (int rc = h->ws.ensure(total)) return rc;
-                goto placed;
-            }
+    bool placed = false;
+    if (total >= (1ul << 30)) {
+        h->ws.release();
+        if (h->ws_vmm.alloc(h->device, total, 64ul << 20, 12345u) == 0) {
             h->ws.p = h->ws_vmm.va;   // not owned by ws (released through ws_vmm)
             h->ws.cap = total;
-            // TDEC_VMM_ORDERS = K > 1: time a one-iteration decode on K chunk orders of
-            // the same physical chunks (remap) and keep the fastest (a full-size
-            // workspace only)
-            const char *ko = getenv("TDEC_VMM_ORDERS");
-            const int K = std::max(1, std::min(32, ko ? atoi(ko) : TDEC_VMM_ORDERS_DEFAULT));
-            if (K > 1 && waves == h->max_waves) {
-                void *planes = nullptr, *bits = nullptr;
-                hipEvent_t e0 = nullptr, e1 = nullptr;
-                const size_t pb = tdec_planes_bytes(h, waves * WAVE), bb = (size_t)waves * WAVE * 2 * h->N * sizeof(int32_t);
-                const bool ok = hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
-                                hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
-                                hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) ==
-                                    hipSuccess;
-                float ms[32];
-                int best = 0;
-                for (int k = 0; ok && k < K; ++k) {
-                    if (k > 0 && h->ws_vmm.remap(12345u + (unsigned)k)) break;
-                    HIPCHK(hipMemsetAsync((char *)h->ws.p + aux_off, 0, WAVE * sizeof(double2), h->stream));
-                    ms[k] = probe_decode_ms(h, waves, (char *)h->ws.p, ck_off, aux_off, (const float *)planes,
-                                            (int32_t *)bits, e0, e1);
-                    if (ms[k] < ms[best]) best = k;
-                    if (getenv("TDEC_PROBE_VERBOSE")) fprintf(stderr, "[tdec] vmm order %d: %.3f ms\n", k, ms[k]);
-                }
-                hipGetLastError();
-                if (e0) hipEventDestroy(e0);
-                if (e1) hipEventDestroy(e1);
-                if (planes) hipFree(planes);
-                if (bits) hipFree(bits);
-                if (ok)
-                    if (int rc = h->ws_vmm.remap(12345u + (unsigned)best)) return rc;
-            }
-            h->le_p = (double2 *)h->ws.p;
-            h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
-            h->aux_p = (double2 *)((char *)h->ws.p + aux_off);
-            HIPCHK(hipMemsetAsync(h->aux_p, 0, WAVE * sizeof(double2), h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            h->ws_waves = waves;
-            return 0;
-        } else if (wa && !strcmp(wa, "contiguous")) {
-            h->ws.release();
-            if (hipExtMallocWithFlags(&h->ws.p, total, hipDeviceMallocContiguous) != hipSuccess) {
-                h->ws.p = nullptr;
-                return fail(TDEC_ENOMEM, "hipExtMallocWithFlags(contiguous) failed (decoder workspace)");
-            }
-            h->ws.cap = total;
-        } else if (int rc = h->ws.ensure(total)) {
-            return rc;
+            placed = true;
+        } else {
+            hipGetLastError();   // no VMM support: one hipMalloc below
         }
-    } else {
-        h->ws.release();
-        const char *pc = getenv("TDEC_PROBE_CANDIDATES");
-        const int per_round = std::max(2, std::min(MAX_CANDIDATES, pc ? atoi(pc) : PROBE_CANDIDATES));
-        int cap = MAX_CANDIDATES;
-        size_t free_b = 0, total_b = 0;   // never let the candidates take more than half of free memory
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::max(1, std::min<int>(cap, (int)(free_b / 2 / total)));
-        void *cand[MAX_CANDIDATES] = {};
-        float ms[MAX_CANDIDATES] = {};
-        int n = 0, best = 0;
-        void *planes = nullptr, *bits = nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        const size_t pb = tdec_planes_bytes(h, waves * WAVE), bb = (size_t)waves * WAVE * 2 * h->N * sizeof(int32_t);
-        bool timed = false;
-        for (int round = 0; round < 2; ++round) {
-            const int first = n, want = std::min(cap, first + (round ? per_round : std::min(per_round, cap / 2 + 1)));
-            for (; n < want; ++n) {
-                if (hipMalloc(&cand[n], total) != hipSuccess) break;
-                hipMemsetAsync((char *)cand[n] + aux_off, 0, WAVE * sizeof(double2), h->stream);
-            }
-            if (n == 0) return fail(TDEC_ENOMEM, "hipMalloc failed (decoder workspace)");
-            if (n == 1) break;
-            if (!timed) {
-                timed = hipMalloc(&planes, pb) == hipSuccess && hipMalloc(&bits, bb) == hipSuccess &&
-                        hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
-                        hipMemsetD32Async((hipDeviceptr_t)planes, 0x3ec00000 /* 0.375f */, pb / 4, h->stream) ==
-                            hipSuccess;
-                if (!timed) break;
-            }
-            for (int i = first; i < n; ++i) {
-                ms[i] = probe_decode_ms(h, waves, (char *)cand[i], ck_off, aux_off, (const float *)planes,
-                                        (int32_t *)bits, e0,
-                                        e1);
-                if (ms[i] < ms[best]) best = i;
-            }
-            float sorted[MAX_CANDIDATES];
-            std::copy(ms + first, ms + n, sorted);
-            std::sort(sorted, sorted + (n - first));
-            const float median = sorted[(n - first) / 2];
-            if (ms[best] <= FAST_VS_MEDIAN * median || n >= cap || n == first) break;   // a fast one, or no room
-        }
-        hipGetLastError();
-        if (getenv("TDEC_PROBE_VERBOSE"))
-            for (int i = 0; i < n; ++i) fprintf(stderr, "[tdec] placement probe %d: %.3f ms%s\n", i, ms[i], i == best ? " *" : "");
-        if (e0) hipEventDestroy(e0);
-        if (e1) hipEventDestroy(e1);
-        if (planes) hipFree(planes);
-        if (bits) hipFree(bits);
-        for (int i = 0; i < n; ++i)
-            if (i != best) hipFree(cand[i]);
-        h->ws.p = cand[best];
-        h->ws.cap = total;
     }
-placed:
+    if (!placed)
+        if (int rc = h->ws.ensure(total)) return rc;
     h->le_p = (double2 *)h->ws.p;
     h->ck_p = (float4 *)((char *)h->ws.p + ck_off);
     h->aux_p = (double2 *)((char *)h->ws.p + aux_off);
@@ -1146,28 +979,6 @@ static int ensure_decl(tdec_t *h, long n_tiles) {
     return 0;
 }
 
-// TDEC_ITEMQ (read per call; build default TDEC_ITEMQ_DEFAULT): the throughput
-// decoders take (tile, iteration) items from per-XCD queues instead of whole tiles
-// per wave (tdec_kernels.hip, DecodeArgs::le2t).
-#ifndef TDEC_ITEMQ_DEFAULT
-#define TDEC_ITEMQ_DEFAULT 0
-#endif
-static bool itemq_on() {
-    const char *e = getenv("TDEC_ITEMQ");
-    return e ? e[0] == '1' : TDEC_ITEMQ_DEFAULT != 0;
-}
-static long iq_cap_of(const tdec_t *h, int tiles) { return std::max(1L, (long)(h->iters - 1) * tiles); }
-// per-tile Le2 ([tiles][N][64] double2), the control block and the rings; the caller
-// has quiesced the handle
-static int ensure_itemq(tdec_t *h, int tiles) {
-    if (tiles <= h->iq_tiles) return 0;
-    if (int rc = h->iq_le2.ensure((size_t)tiles * h->N * WAVE * sizeof(double2))) return rc;
-    if (int rc = h->iq_ctl.ensure(32 * 9 * sizeof(int))) return rc;
-    if (int rc = h->iq_ring.ensure((size_t)8 * iq_cap_of(h, tiles) * sizeof(int))) return rc;
-    h->iq_tiles = tiles;
-    return 0;
-}
-
 int tdec_reserve(tdec_t *h, int max_batch) {
     if (!h || max_batch < 0) return fail(TDEC_EINVAL, "bad reserve");
     if (max_batch == 0) return 0;
@@ -1185,11 +996,9 @@ int tdec_reserve(tdec_t *h, int max_batch) {
     if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap ||
         n_tiles_of(max_batch) > h->decl_tiles)
         quiesce(h);   // regrowth frees
-    if (itemq_on() && n_tiles_of(max_batch) > h->iq_tiles) quiesce(h);
     int rc = ensure_ws(h, want_waves);
     if (!rc) rc = h->planes_own.ensure(tdec_planes_bytes(h, max_batch));
     if (!rc) rc = ensure_decl(h, n_tiles_of(max_batch));
-    if (!rc && itemq_on()) rc = ensure_itemq(h, n_tiles_of(max_batch));
     if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
     return rc;
 }
@@ -1242,21 +1051,11 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
     if (int rc = order_on(h, st)) return rc;
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     if (h->d_simd_prog && hipMemsetAsync(h->d_simd_prog, 0, SIMD_PROG_BYTES, st) == hipSuccess) a.simd_prog = h->d_simd_prog;
-    if (itemq_on() && tiles <= h->iq_tiles) {   // reserved by tdec_reserve; otherwise whole tiles per wave
-        HIPCHK(hipMemsetAsync(h->iq_ctl.p, 0, 32 * 9 * sizeof(int), st));
-        HIPCHK(hipMemsetAsync(h->iq_ring.p, 0, (size_t)8 * iq_cap_of(h, tiles) * sizeof(int), st));
-        a.le2t = (double2 *)h->iq_le2.p;
-        a.iq_ctl = (int *)h->iq_ctl.p;
-        a.iq_ring = (int *)h->iq_ring.p;
-        a.iq_cap = (int)iq_cap_of(h, tiles);
-        a.tile_ctr = nullptr;
-    } else {
-        a.tail_flag = h->d_tail;
-        a.tail_seq = ++h->tail_seq;
-    }
+    a.tail_flag = h->d_tail;
+    a.tail_seq = ++h->tail_seq;
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
     hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(DEC_BLOCK), 0, st,
@@ -1286,17 +1085,13 @@ int tdec_decode_batch_dev(tdec_t *h, int B, const float *d_llr, long llr_stride,
     return rc;
 }
 
-// Zero-copy single calls (TDEC_ZC=0 turns them off; read per call): a small
-// host-pointer call of at most ZC_MAX_ROWS rows lets the kernels read their
+// Zero-copy single calls: a small host-pointer call of at most ZC_MAX_ROWS rows lets the kernels read their
 // inputs from, and write their outputs to, the page-locked staging buffer itself
 // instead of a DMA each way.  Measured (profiles/r04y/, r04z/): bcjr_max_log_map
 // at N = 752 0.065 vs 0.073 ms, one decode() 0.306 vs 0.317 ms, 16 codewords
 // 0.352 vs 0.366 ms, 64 even (0.404 vs 0.41), 256 slower (0.677 vs 0.618).
 constexpr int ZC_MAX_ROWS = 64;
-static bool zero_copy(int B) {
-    const char *e = getenv("TDEC_ZC");
-    return B <= ZC_MAX_ROWS && !(e && e[0] == '0');
-}
+static bool zero_copy(int B) { return B <= ZC_MAX_ROWS; }
 
 
 // Host-pointer decode in chunks, so device memory stays bounded for any B:
@@ -1628,12 +1423,13 @@ static int siso_batch_impl(tdec_t *h, int B, const T *LcA, const T *LcB, const T
 // float32 channel-LLR row uses the first half of its slot.
 static size_t siso_slot(const tdec_t *h, int rows) { return ((size_t)rows * h->N * 8 + 255) / 256 * 256; }
 
-// TDEC_SPIN (read per call; default on): a zero-copy staged call waits for the frame
-// SISO's completion counter in the page-locked buffer instead of the stream.
-static bool spin_wait() {
-    const char *e = getenv("TDEC_SPIN");
-    return !(e && e[0] == '0');
-}
+// A zero-copy staged call waits for the frame SISO's per-row completion flags
+// (coherent, mapped host memory) instead of the stream: the rows' outputs are in
+// the page-locked slots once every flag holds the call's sequence number (a row
+// sets its flag after a system-scope release of its stores).  The wait is bounded
+// in time (SPIN_LIMIT_S); past it the call falls back to a stream wait and counts
+// the fallback (tdec_siso_stats), which the GPU tests require to stay at zero.
+constexpr double SPIN_LIMIT_S = 0.25;
 
 template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
     constexpr bool F64 = sizeof(T) == 8;
@@ -1656,24 +1452,25 @@ template <typename T> static int siso_staged_impl(tdec_t *h, int B, double sf) {
         dp = (char *)h->h_misc.p;
         HIPCHK(hipMemcpyAsync(dp, h->pin_siso.p, 6 * sl, hipMemcpyHostToDevice, s));
     }
-    volatile unsigned *flags = (volatile unsigned *)((char *)h->pin_siso.p + 8 * sl);
-    const bool spin = zc && spin_wait();
+    volatile unsigned *flags = (volatile unsigned *)h->pin_flags.p;
+    const bool spin = zc && h->pin_flags.dev;
     if (spin && ++h->siso_seq == 0) h->siso_seq = 1;   // flags start at 0: never a valid sequence number
     if ((rc = siso_launch<T>(h, B, (const T *)dp, (const T *)(dp + sl), (const T *)(dp + 2 * sl), (const T *)(dp + 3 * sl),
                              (const double *)(dp + 4 * sl), (const double *)(dp + 5 * sl), sf, (double *)(dp + 6 * sl),
-                             (double *)(dp + 7 * sl), fr, spl, s, spin ? (unsigned *)(dp + 8 * sl) : nullptr)))
+                             (double *)(dp + 7 * sl), fr, spl, s, spin ? (unsigned *)h->pin_flags.dev : nullptr)))
         return rc;
     if (spin) {
-        // The rows' outputs are in the page-locked slots once every row's flag holds
-        // this call's sequence number (a row sets it after fencing its stores).  The
-        // kernel may still be retiring when this returns; later work on the handle's
-        // stream is ordered behind it and nothing it touches afterwards is the
-        // caller's.  A kernel that never sets them (a fault) is caught by the stream
-        // wait after ~2^26 polls.
-        long polls = 0;
+        // The kernel may still be retiring when this returns; later work on the
+        // handle's stream is ordered behind it and nothing it touches afterwards is
+        // the caller's.  A kernel that never sets the flags (a fault) is caught by
+        // the stream wait once the time limit has passed.
+        const auto t0 = std::chrono::steady_clock::now();
+        unsigned polls = 0;
         for (int r = 0; r < B; ++r)
             while (flags[r] != h->siso_seq) {
-                if (++polls > (1L << 26)) {
+                if ((++polls & 1023u) == 0 &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > SPIN_LIMIT_S) {
+                    ++h->siso_fallbacks;
                     HIPCHK(hipStreamSynchronize(s));
                     if (flags[r] != h->siso_seq) return fail(TDEC_EHIP, "frame SISO finished without flagging its rows");
                     break;
@@ -1700,11 +1497,14 @@ int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes) {
         quiesce(h);
         HIPCHK(hipStreamSynchronize(h->stream));   // a flag-waited call's kernel may still be retiring
         h->pin_siso.release();   // the caller's views of the old buffer die with this call
+        h->pin_flags.release();
         h->siso_rows = 0;
-        // + the per-row completion flags
-        if (int rc = h->pin_siso.ensure(8 * siso_slot(h, rows) + ((size_t)rows * 4 + 255) / 256 * 256)) return rc;
+        if (int rc = h->pin_siso.ensure(8 * siso_slot(h, rows))) return rc;
+        // the per-row completion flags (coherent: polled while the kernel runs)
+        if (int rc = h->pin_flags.ensure(((size_t)rows * 4 + 255) / 256 * 256, hipHostMallocCoherent | hipHostMallocMapped))
+            return rc;
         h->siso_rows = rows;
-        std::memset((char *)h->pin_siso.p + 8 * siso_slot(h, rows), 0, (size_t)rows * 4);
+        std::memset(h->pin_flags.p, 0, (size_t)rows * 4);
     }
     *buf = h->pin_siso.p;
     *slot_bytes = siso_slot(h, h->siso_rows);
@@ -1713,6 +1513,12 @@ int tdec_siso_staging(tdec_t *h, int rows, void **buf, size_t *slot_bytes) {
 
 int tdec_siso_staged(tdec_t *h, int B, int lc_f64, double sf) {
     return lc_f64 ? siso_staged_impl<double>(h, B, sf) : siso_staged_impl<float>(h, B, sf);
+}
+
+int tdec_siso_stats(const tdec_t *h, long *flag_fallbacks) {
+    if (!h || !flag_fallbacks) return fail(TDEC_EINVAL, "bad siso stats arguments");
+    *flag_fallbacks = h->siso_fallbacks;
+    return 0;
 }
 
 int tdec_siso_batch(tdec_t *h, int B, const float *LcA, const float *LcB, const float *LcW, const float *LcY,
@@ -1863,19 +1669,11 @@ int tdec_demap_planes_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
         HIPCHK(hipMemsetAsync(h->d_decl_n, 0, sizeof(unsigned), st));
         HIPCHK(hipMemsetAsync(h->d_decl_ovf, 0, (size_t)n_tiles, st));
     }
-    // TDEC_DM_PERSIST: one round of resident blocks (occupancy of this instance; the
-    // same device type throughout a process)
-    auto grid_of = [&](const void *kern, int) {
-        int bpc = 0;
-        if (TDEC_DM_PERSIST && hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, BLOCK, 0) != hipSuccess)
-            bpc = -1;
-        const long resident = TDEC_DM_PERSIST && bpc > 0 ? (long)bpc * std::max(1, h->n_cu) : n_items;
-        return dim3((unsigned)std::min(n_items, resident));
-    };
+    const dim3 grid((unsigned)n_items);   // one block per item
     const dim3 fgrid((unsigned)std::max<long>(1, std::min<long>(n_tiles, 1024)));
     switch (bps) {
 #define LAUNCH_PLANES(TT, K, SP, F64)                                                                     \
-    hipLaunchKernelGGL((k_demap_planes<TT, K, SP>), grid_of((const void *)k_demap_planes<TT, K, SP>, F64), dim3(BLOCK), \
+    hipLaunchKernelGGL((k_demap_planes<TT, K, SP>), grid, dim3(BLOCK),                                  \
                        0, st, B, h->N, S, d_syms, (const TT *)h->cons.buf.p, c, (const int *)h->d_src,          \
                        (const int *)h->d_off, n_avail, P, n_items, dd)
 #define CASE(K)                                                                                              \
@@ -2030,7 +1828,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     hipStream_t st = (hipStream_t)stream;
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
-    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used, h->row_pad,
+    DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,

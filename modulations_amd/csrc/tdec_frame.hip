@@ -44,17 +44,15 @@ namespace tdec {
 
 constexpr int FR_WAVES = 8;
 constexpr int FR_BLOCK = FR_WAVES * WAVE;
-// TDEC_FR_WPD: waves per direction in the recursions (1, 2 or 4; see fr_recursion_x).
-// Measured (profiles/r04e/ab_frame_*, decode of N = 752 r = 1/2): 0.30 vs 0.34 ms
-// at B = 1, 0.36 vs 0.38 ms at B = 64, 1.40 vs 1.50 ms at B = 1 024: the default.
-// Four waves per direction (16 segments) halve phase A but need 5.1 rounds per SISO
-// instead of 2.8 and lose: 0.36 vs 0.29 ms at B = 1, 1.80 vs 1.39 ms at B = 1 024
-// (profiles/r04m/).
-#ifndef TDEC_FR_WPD
-#define TDEC_FR_WPD 2
-#endif
-constexpr int FR_NSEG_MAX = TDEC_FR_WPD == 4 ? 16 : 8;   // segments per direction at most
-// TDEC_FR_LMIN: segments per direction = N / TDEC_FR_LMIN (at least 1, at most the
+// Waves per direction in the recursions: 1 or 2 (WPD, chosen per block length by
+// tdec_api.hip fr_wpd; see fr_recursion_x).  Two measured faster than one at N = 752
+// (profiles/r04e/ab_frame_*, decode of N = 752 r = 1/2: 0.30 vs 0.34 ms at B = 1,
+// 0.36 vs 0.38 ms at B = 64, 1.40 vs 1.50 ms at B = 1 024).  Four waves per direction
+// (16 segments) halve phase A but need 5.1 rounds per SISO instead of 2.8 and lose:
+// 0.36 vs 0.29 ms at B = 1, 1.80 vs 1.39 ms at B = 1 024 (profiles/r04m/).
+constexpr int FR_WPD_MAX = 2;
+constexpr int FR_NSEG_MAX = 8;   // segments per direction at most (4 per wave)
+// Segments per direction = N / FR_LMIN (at least 1, at most the
 // P the waves provide), the steps split evenly over them in whole 4-step blocks.
 // A segment shorter than the recursions' typical merge depth (~40 steps) rarely
 // merges in its first re-run, so the rounds hand end vectors down a chain of
@@ -65,11 +63,9 @@ constexpr int FR_NSEG_MAX = TDEC_FR_WPD == 4 ? 16 : 8;   // segments per directi
 // least 32 steps per segment gives 32 + 32 (one wave per direction,
 // profiles/r05/lmin_wpd1/: N = 64 0.150 -> 0.123 ms) and the same segments at
 // every other block size.
-#ifndef TDEC_FR_LMIN
-#define TDEC_FR_LMIN 32
-#endif
+constexpr int FR_LMIN = 32;
 __host__ __device__ constexpr int fr_seg_len(int N, int P) {
-    int n = N / TDEC_FR_LMIN;
+    int n = N / FR_LMIN;
     n = n < 1 ? 1 : (n > P ? P : n);
     return (N + 4 * n - 1) / (4 * n) * 4;
 }
@@ -160,49 +156,17 @@ template <int DIR> __device__ __forceinline__ FrLane<DIR> fr_lane(int l) {
     return L;
 }
 
-// v of lane l ^ (8 >> PH) within the 16-lane row
-template <int PH> __device__ __forceinline__ float fr_xchg(float v) {
-    const int i = __float_as_int(v);
-    if constexpr (PH == 0) return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x128, 0xF, 0xF, false));   // row_ror:8
-    if constexpr (PH == 1) {   // lanes of banks 0, 2 read l + 4 (row_shl:4), banks 1, 3 read l - 4 (row_shr:4)
-        const int t = __builtin_amdgcn_mov_dpp(i, 0x104, 0xF, 0x5, false);
-        return __int_as_float(__builtin_amdgcn_update_dpp(t, i, 0x114, 0xF, 0xA, false));
-    }
-    if constexpr (PH == 2) return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
-    return __int_as_float(__builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false));                           // quad_perm [1,0,3,2]
-}
-// TDEC_FR_UNI: the round's lane mask in SGPRs (uni64)
-#ifndef TDEC_FR_UNI
-#define TDEC_FR_UNI 1
-#endif
-// TDEC_FR_EXP (timing experiments only, WRONG RESULTS): 1 = no vector stores in the
-// fast blocks, 2 = no pair-maxima loads for the next block, 4 = no step (the
-// vector passes through)
-#ifndef TDEC_FR_EXP
-#define TDEC_FR_EXP 0
-#endif
 // one trellis step (:165-179 / :203-213 with pair maxima): max over the two branch
-// pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row)
-// TDEC_FR_N0 (build variant): every lane also forms state 0's new value itself, from lane
-// 0 and its partner lane 8 >> PH (state 0's two predecessors / successors in both
-// labellings) with state 0's pair maxima pm[0] / pm[7] -- the same operands in
-// the same order as lane 0, so the same bits -- instead of waiting for lane 0's
-// result through a second DPP move: the chain is DPP-add, max3, subtract.
-// Measured slower (profiles/r04e/ab_frame_*: 0.39 vs 0.34 ms per decode at B = 1,
-// 1.70 vs 1.50 ms at B = 1 024): the extra VALU work outweighs the shorter chain.
-#ifndef TDEC_FR_N0
-#define TDEC_FR_N0 0
-#endif
-// TDEC_FR_ASM: the partner's add and the normalisation as DPP forms of the VALU
-// ops themselves (v_add_f32_dpp: partner + po; v_subrev_f32_dpp: n - n[lane 0]),
-// not a DPP move feeding them -- 2 fewer instructions on the serial chain (3 in
-// the xor-4 phase).  Same IEEE operations, so the same bits.  The s_nop 1 covers
-// the VALU-write -> DPP-read hazard (2 wait states), which the compiler does not
-// track through inline asm.  Measured 0.34 vs 0.35 ms per decode at B = 1, 1.50
-// vs 1.52 ms at B = 1 024 (profiles/r04e/ab_frame_*).
-#ifndef TDEC_FR_ASM
-#define TDEC_FR_ASM 1
-#endif
+// pairs into the lane's new state, from -1e9, minus state 0 (lane 0 of the row).
+// The partner's add and the normalisation are DPP forms of the VALU ops themselves
+// (v_add_f32_dpp: partner + po; v_subrev_f32_dpp: n - n[lane 0]), not a DPP move
+// feeding them -- 2 fewer instructions on the serial chain (3 in the xor-4 phase).
+// Same IEEE operations, so the same bits.  The s_nop 1 covers the VALU-write ->
+// DPP-read hazard (2 wait states), which the compiler does not track through
+// inline asm.  Measured 0.34 vs 0.35 ms per decode at B = 1, 1.50 vs 1.52 ms at B =
+// 1 024 (profiles/r04e/ab_frame_*).  (Every lane forming state 0's new value itself
+// instead of waiting for lane 0's through a second DPP move measured slower: 0.39
+// vs 0.34 ms.)
 template <int PH> __device__ __forceinline__ float fr_partner_add(float v, float po) {
     float y;
     if constexpr (PH == 0)
@@ -217,23 +181,12 @@ template <int PH> __device__ __forceinline__ float fr_partner_add(float v, float
         asm("s_nop 1\n\tv_add_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(y) : "v"(v), "v"(po));
     return y;
 }
-template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po, float pa, float pb) {
-    if constexpr ((TDEC_FR_EXP & 4) != 0) return v + ps;
-    if constexpr (TDEC_FR_ASM && !TDEC_FR_N0) {
-        const float y = fr_partner_add<PH>(v, po);
-        const float n = fmaxf(fmaxf(NEG, v + ps), y);
-        float r;
-        asm("s_nop 1\n\tv_subrev_f32_dpp %0, %1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(n));
-        return r;
-    }
-    const float o = fr_xchg<PH>(v);
-    const float n = fmaxf(fmaxf(NEG, v + ps), o + po);
-    if constexpr (TDEC_FR_N0) {
-        const float v0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150, 0xF, 0xF, false));
-        const float v8 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + (8 >> PH), 0xF, 0xF, false));
-        return n - fmaxf(fmaxf(NEG, v0 + pa), v8 + pb);
-    }
-    return n - __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));   // row_newbcast:0
+template <int PH> __device__ __forceinline__ float fr_step(float v, float ps, float po) {
+    const float y = fr_partner_add<PH>(v, po);
+    const float n = fmaxf(fmaxf(NEG, v + ps), y);
+    float r;
+    asm("s_nop 1\n\tv_subrev_f32_dpp %0, %1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(n));
+    return r;
 }
 
 // log-MAP (ALGO 1): the same step with max* (jac, tdec_kernels.hip) over the lane's
@@ -248,77 +201,26 @@ template <int PH> __device__ __forceinline__ float fr_step_lm(float v, float ps,
     asm("s_nop 1\n\tv_subrev_f32_dpp %0, %1, %1 row_newbcast:0 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(n));
     return r;
 }
-template <int ALGO, int PH> __device__ __forceinline__ float fr_step_a(float v, const float (&c)[4]) {
+template <int ALGO, int PH> __device__ __forceinline__ float fr_step_a(float v, const float (&c)[2]) {
     if constexpr (ALGO == 1) return fr_step_lm<PH>(v, c[0], c[1]);
-    else return fr_step<PH>(v, c[0], c[1], c[2], c[3]);
+    else return fr_step<PH>(v, c[0], c[1]);
 }
 
-// TDEC_FR_ASMBLK: a fast block (4 steps, each entering vector stored) as one asm
-// sequence -- the same instructions as fr_step / lds_st (own add, DPP partner add,
-// v_max3 with -1e9, DPP normalisation by lane 0), so the same bits, with each store
-// and the next step's own add placed in the DPP read-after-write hazard slots
-// instead of s_nop, and no per-step s_waitcnt (the stores are not waited on here;
-// the compiler's later waits count only its own LDS operations, which retire in
-// order before these, so they stay conservative).  a[ph]: LDS byte address of the
-// vector entering step ph.  Measured 0.28 vs 0.29 ms per decode at B = 1, 1.33 vs
-// 1.37 ms at B = 1 024, same bits (profiles/r04s/).
-#ifndef TDEC_FR_ASMBLK
-#define TDEC_FR_ASMBLK 1
-#endif
-__device__ __forceinline__ void fr_block_asm(float &v, const float (&c)[4][4], unsigned a0, unsigned a1, unsigned a2,
-                                             unsigned a3) {
-    float t, u, n;
-    asm volatile(
-        "ds_write_b32 %[a0], %[v]\n\t"
-        "v_add_f32 %[u], %[v], %[c00]\n\t"
-        "s_nop 1\n\t"
-        "v_add_f32_dpp %[t], %[v], %[c01] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
-        "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"
-        "s_nop 1\n\t"
-        "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "ds_write_b32 %[a1], %[v]\n\t"
-        "v_add_f32 %[u], %[v], %[c10]\n\t"
-        "v_add_f32_dpp %[t], %[v], %[c11] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
-        "v_add_f32_dpp %[t], %[v], %[c11] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
-        "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"
-        "s_nop 1\n\t"
-        "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "ds_write_b32 %[a2], %[v]\n\t"
-        "v_add_f32 %[u], %[v], %[c20]\n\t"
-        "v_add_f32_dpp %[t], %[v], %[c21] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-        "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"
-        "s_nop 1\n\t"
-        "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "ds_write_b32 %[a3], %[v]\n\t"
-        "v_add_f32 %[u], %[v], %[c30]\n\t"
-        "v_add_f32_dpp %[t], %[v], %[c31] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_max3_f32 %[n], %[u], %[neg], %[t]\n\t"
-        "s_nop 1\n\t"
-        "v_subrev_f32_dpp %[v], %[n], %[n] row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1"
-        : [v] "+v"(v), [t] "=&v"(t), [u] "=&v"(u), [n] "=&v"(n)
-        : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [c00] "v"(c[0][0]), [c01] "v"(c[0][1]),
-          [c10] "v"(c[1][0]), [c11] "v"(c[1][1]), [c20] "v"(c[2][0]), [c21] "v"(c[2][1]), [c30] "v"(c[3][0]),
-          [c31] "v"(c[3][1]), [neg] "s"(NEG)
-        : "memory");
-}
-
-// TDEC_FR_BLK8: fast blocks of 8 steps (two labelling periods) instead of 4 --
-// the same instructions per step as fr_block_asm, with the block's control
-// (run-mask and end tests, the merge compare, address updates, the next block's
-// pair-maxima loads) paid once per 8 steps.  a[ph]: LDS byte address of the
-// vector entering step ph of the block's LOWER-addressed half (alpha: steps
-// 0-3 at +0, 4-7 at +256; beta, whose rows descend: steps 0-3 at +256, 4-7 at +0),
-// c[j]: step j's own / partner pair maxima.
-#ifndef TDEC_FR_BLK8
-#define TDEC_FR_BLK8 1
-#endif
-// TDEC_FR_BLK8_LM: the log-MAP recursion in the same 8-step blocks, as C++ steps
-// (profiles/r05/frame_lm8/: log-MAP decode() per frame N = 752 r = 1/2 1.085 ->
-// 0.916 ms, N = 48 0.200 -> 0.178 ms; same bits)
-#ifndef TDEC_FR_BLK8_LM
-#define TDEC_FR_BLK8_LM 1
-#endif
+// Fast blocks of 8 steps (two labelling periods), max-log as one asm sequence: the
+// same instructions as fr_step / lds_st (own add, DPP partner add, v_max3 with -1e9,
+// DPP normalisation by lane 0), so the same bits, with each store and the next
+// step's own add placed in the DPP read-after-write hazard slots instead of s_nop,
+// no per-step s_waitcnt (the stores are not waited on here; the compiler's later
+// waits count only its own LDS operations, which retire in order before these, so
+// they stay conservative), and the block's control (run-mask and end tests, the
+// merge compare, address updates, the next block's pair-maxima loads) paid once per
+// 8 steps.  a[ph]: LDS byte address of the vector entering step ph of the block's
+// LOWER-addressed half (alpha: steps 0-3 at +0, 4-7 at +256; beta, whose rows
+// descend: steps 0-3 at +256, 4-7 at +0), c[j]: step j's own / partner pair maxima.
+// (4-step asm blocks: 0.28 vs 0.29 ms per decode at B = 1 against C++ steps,
+// profiles/r04s/; 8-step blocks faster again, round 5.)  log-MAP runs the same
+// 8-step blocks as C++ steps (profiles/r05/frame_lm8/: log-MAP decode() per frame
+// N = 752 r = 1/2 1.085 -> 0.916 ms, N = 48 0.200 -> 0.178 ms; same bits).
 #define FR8_STEP0(A, OFF, CO, CP, NOP)                                                          \
     "ds_write_b32 %[" A "], %[v] offset:" OFF "\n\t"                                          \
     "v_add_f32 %[u], %[v], %[" CO "]\n\t" NOP                                                 \
@@ -416,89 +318,14 @@ template <int DIR, bool CMP, int ALGO = 0>
 __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrLane<DIR> &L, int g, int lane, int u0,
                                                        int len, unsigned long long run, float v, int stat) {
     const int N = R.N;
-    if (TDEC_FR_UNI) run = uni64(run);
+    run = uni64(run);
     // byte offsets of the rows of step U: store row (alpha[U] / beta[N - U]) and pm row (position)
     auto srow = [&](int U) { return (DIR ? N - U : U) * 64; };
     auto prow = [&](int U) { return (DIR ? N - 1 - U : U) * 32; };
-    lds_b *const sink_s = R.sink + (DIR ? 256 : 0);
     unsigned long long reached = 0;
-    float pc[4][4], pn[4][4] = {};   // per phase: the lane's own / partner pair maxima, state 0's pm[0] / pm[7]
     float cmpv = 0.0f, cmpn = 0.0f;
-    // 8-step blocks: max-log as one asm sequence, log-MAP (TDEC_FR_BLK8_LM) as C++ steps
-    constexpr bool B8 = TDEC_FR_BLK8 && !TDEC_FR_N0 && !TDEC_FR_EXP &&
-                        (ALGO == 0 ? TDEC_FR_ASMBLK && TDEC_FR_ASM : TDEC_FR_BLK8_LM != 0);
-    if constexpr (!B8) {
-        const lds_b *pr = R.pmt + prow(u0);
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {
-            pc[ph][0] = lds_ld(pr + L.poff[ph][0]);
-            pc[ph][1] = lds_ld(pr + L.poff[ph][1]);
-            if constexpr (TDEC_FR_N0) {
-                pc[ph][2] = lds_ld(pr + (DIR ? -32 : 32) * ph);
-                pc[ph][3] = lds_ld(pr + (DIR ? -32 : 32) * ph + 28);
-            }
-        }
-    }
     if constexpr (CMP) cmpv = lds_ld(R.st + srow(u0) + L.soff[0]);
-    // one block of 4 steps from pair maxima `c` while the next block's go to `n`
-    // (ping-pong over two register sets: no moves between blocks)
-    auto block = [&](int u, float (&c)[4][4], float (&n)[4][4], float &cv, float &cn) -> bool {
-#if TDEC_FR_STATS == 1
-        if (lane == 0) atomicAdd(&g_fr_stats[stat], 1ull);
-#endif
-        if constexpr (CMP) run &= ~grp_all16(__ballot(v == cv));   // merged: the rest is stored already
-        if (!run) return false;
-        const int U = u0 + u;
-        // the next block's pair maxima and compare value (rows past the end are read, unused)
-        if (!(TDEC_FR_EXP & 2)) {
-            const lds_b *pr = R.pmt + prow(U + 4);
-#pragma unroll
-            for (int ph = 0; ph < 4; ++ph) {
-                n[ph][0] = lds_ld(pr + L.poff[ph][0]);
-                n[ph][1] = lds_ld(pr + L.poff[ph][1]);
-                if constexpr (TDEC_FR_N0) {
-                    n[ph][2] = lds_ld(pr + (DIR ? -32 : 32) * ph);
-                    n[ph][3] = lds_ld(pr + (DIR ? -32 : 32) * ph + 28);
-                }
-            }
-            if constexpr (CMP) cn = lds_ld(R.st + srow(U + 4) + L.soff[0]);
-        }
-        const bool rl = (run >> lane) & 1;
-        lds_b *const srw = R.st + srow(U);
-        if (!(__ballot(u + 4 >= len) & run)) {   // every running group has steps after this block
-            lds_b *const sr = rl ? srw : sink_s;
-            if constexpr (ALGO == 0 && TDEC_FR_ASMBLK && TDEC_FR_ASM && !TDEC_FR_N0 && !TDEC_FR_EXP) {
-                fr_block_asm(v, c, (unsigned)(uintptr_t)(sr + L.soff[0]), (unsigned)(uintptr_t)(sr + L.soff[1]),
-                             (unsigned)(uintptr_t)(sr + L.soff[2]), (unsigned)(uintptr_t)(sr + L.soff[3]));
-            } else {
-                if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[0], v);
-                v = fr_step_a<ALGO, 0>(v, c[0]);
-                if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[1], v);
-                v = fr_step_a<ALGO, 1>(v, c[1]);
-                if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[2], v);
-                v = fr_step_a<ALGO, 2>(v, c[2]);
-                if (!(TDEC_FR_EXP & 1)) lds_st(sr + L.soff[3], v);
-                v = fr_step_a<ALGO, 3>(v, c[3]);
-            }
-        } else {   // some group ends in this block: per-step bounds, end vector captured
-            lds_b *const evg = R.ev + g * 64;
-#define FR_SLOW_STEP(PH)                                                       \
-    {                                                                          \
-        const int uu = u + PH;                                                 \
-        if (rl && uu < len) lds_st(srw + L.soff[PH], v);                       \
-        const float vn = fr_step_a<ALGO, PH>(v, c[PH]);                             \
-        if (rl && uu == len - 1) lds_st(evg + 4 * L.lbl[(PH + 1) & 3], vn);    \
-        v = vn;                                                                \
-    }
-            FR_SLOW_STEP(0) FR_SLOW_STEP(1) FR_SLOW_STEP(2) FR_SLOW_STEP(3)
-#undef FR_SLOW_STEP
-            const unsigned long long ended = __ballot(u + 4 >= len) & run;
-            reached |= ended;
-            run &= ~ended;
-        }
-        return true;
-    };
-    if constexpr (B8) {
+    {
         // 8-step blocks: the pair maxima of 8 steps from the block's two row halves
         // (alpha: rows U, U + 4 ascending; beta: its rows descend, so the lower half
         // U + 4 is the base and U sits 4 rows above it)
@@ -530,7 +357,7 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
                     for (int j = 0; j < 8; ++j) {
                         const int h = j >> 2, hoff = DIR ? (h ? 0 : 256) : (h ? 256 : 0);
                         lds_st(sr + hoff + L.soff[j & 3], v);
-                        const float c4[4] = {c[j][0], c[j][1], 0.0f, 0.0f};
+                        const float c4[2] = {c[j][0], c[j][1]};
                         switch (j & 3) {
                         case 0: v = fr_step_a<ALGO, 0>(v, c4); break;
                         case 1: v = fr_step_a<ALGO, 1>(v, c4); break;
@@ -545,10 +372,7 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
                 for (int j = 0; j < 8; ++j) {
                     const int uu = u + j;
                     lds_b *const rw = R.st + srow(U + (j & 4));
-                    float c4[4];
-                    c4[0] = c[j][0];
-                    c4[1] = c[j][1];
-                    c4[2] = c4[3] = 0.0f;
+                    const float c4[2] = {c[j][0], c[j][1]};
                     if (rl && uu < len) lds_st(rw + L.soff[j & 3], v);
                     float vn;
                     switch (j & 3) {
@@ -572,12 +396,8 @@ __device__ __forceinline__ unsigned long long fr_round(const FrRec &R, const FrL
             if (!block8(u, qc, qn, cmpv, cmpn)) break;
             if (!block8(u + 8, qn, qc, cmpn, cmpv)) break;
         }
-        return reached;
     }
-    for (int u = 0;; u += 8) {
-        if (!block(u, pc, pn, cmpv, cmpn)) break;
-        if (!block(u + 4, pn, pc, cmpn, cmpv)) break;
-    }
+    (void)stat;
     return reached;
 }
 
@@ -648,7 +468,7 @@ template <int DIR, int ALGO = 0> __device__ void fr_recursion(const FrRec &R, in
     }
 }
 
-// ---- TDEC_FR_WPD 2 / 4: 8 / 16 segments per direction on two / four waves each -----------
+// ---- WPD 2: 8 segments per direction on two waves each -------------------------------------
 // The same rounds as fr_recursion, with the segments of one direction spread over
 // two waves (alpha: waves 0-1, beta: waves 2-3), so each round is a workgroup step:
 // every wave (the idle ones too) passes three barriers per round -- starts read
@@ -661,8 +481,7 @@ enum { FR_A = 0, FR_FIX1 = 1, FR_FIXN = 2, FR_P2S = 3, FR_P2 = 4 };
 template <int ALGO = 0> __device__ void fr_recursion_x(lds_b *sm, const FrLds &Lo, int N, int wave, int lane) {
     volatile __attribute__((address_space(3))) FrCtl *ctl =
         (volatile __attribute__((address_space(3))) FrCtl *)(sm + Lo.ev + 2 * FR_NSEG_MAX * 64);
-    constexpr int WPDX = TDEC_FR_WPD > 1 ? TDEC_FR_WPD : 2;   // waves per direction
-    static_assert(WPDX == 2 || WPDX == 4, "TDEC_FR_WPD: 1, 2 or 4");
+    constexpr int WPDX = 2;   // waves per direction
     const int Ls = fr_seg_len(N, 4 * WPDX);   // segment length (a multiple of 4)
     const int nseg = (N + Ls - 1) / Ls;     // 1..4 * WPDX
     const unsigned all = (1u << nseg) - 1;
@@ -912,7 +731,7 @@ __device__ void fr_siso(const In &in, const Out &out, const int (&pos)[FR_J], co
 #if TDEC_FR_STATS
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // R: alpha on wave 0, beta on wave 1 (TDEC_FR_WPD 2: alpha on waves 0-1, beta on 2-3)
+    // R: alpha on wave 0, beta on wave 1 (WPD 2: alpha on waves 0-1, beta on 2-3)
     if constexpr (WPD == 1) {
         if (wave == 0) fr_recursion<0, ALGO>(FrRec{sm + Lo.st_a, pmt, sm + Lo.ev, sm + Lo.sink, N}, lane);
         else if (wave == 1) fr_recursion<1, ALGO>(FrRec{sm + Lo.st_b, pmt, sm + Lo.ev + FR_NSEG_MAX * 64, sm + Lo.sink + 512, N}, lane);
@@ -972,7 +791,7 @@ struct FrArgs {
 // LG: Le2 in global scratch (N > 805; see fr_lds).  WPD: waves per recursion
 // direction (1: one wave, segments and rounds inside it, no cross-wave barriers;
 // 2: fr_recursion_x), chosen per call by N (tdec_api.hip fr_wpd).
-template <bool LG, int ALGO = 0, int WPD = TDEC_FR_WPD>
+template <bool LG, int ALGO = 0, int WPD = FR_WPD_MAX>
 __global__ __launch_bounds__(FR_BLOCK) void k_turbo_decode_frame(FrArgs p, const int *__restrict__ perm,
                                                                  const int *__restrict__ inv,
                                                                  const int *__restrict__ ord) {
@@ -1053,7 +872,7 @@ struct FrSisoArgs {
     unsigned *done;   // nullable: host-mapped per-row completion flags, set to seq after the row's outputs
     unsigned seq;
 };
-template <typename T, int ALGO = 0, int WPD = TDEC_FR_WPD>
+template <typename T, int ALGO = 0, int WPD = FR_WPD_MAX>
 __global__ __launch_bounds__(FR_BLOCK) void k_siso_frame(FrSisoArgs p) {
     extern __shared__ float4 fr_sm[];
     lds_b *sm = (lds_b *)fr_sm;

@@ -128,15 +128,7 @@ __device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two IEEE f32 ops per lane
 
-// TDEC_LM_FAST (timing experiment, DIFFERENT BITS from the oracle): the same max*
-// without the +8 that bounds the instruction's argument grid, max + log2(1 +
-// 2^-|a-b|) (one VALU operation fewer per max*, two per lse4) -- measures what the
-// bit-exact pinning of the hardware primitives costs.
-#ifndef TDEC_LM_FAST
-#define TDEC_LM_FAST 0
-#endif
 __device__ __forceinline__ float jac(float a, float b) {
-    if constexpr (TDEC_LM_FAST) return fmaxf(a, b) + hw_log2(1.0f + hw_exp2(-fabsf(a - b)));
     const float t = fabsf(a - b) + LM_C;
     const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
     return fmaxf(a, b) + hw_log2(w);
@@ -146,45 +138,12 @@ __device__ __forceinline__ float jac(float a, float b) {
 // order by fma, plus Mc - 8 (exact: the maximum rounded to Mc's grid, the shift
 // the terms were taken against).
 __device__ __forceinline__ float lse4(float x0, float x1, float x2, float x3) {
-    if constexpr (TDEC_LM_FAST) {
-        const float M = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3));
-        return M + hw_log2(((hw_exp2(x0 - M) + hw_exp2(x1 - M)) + hw_exp2(x2 - M)) + hw_exp2(x3 - M));
-    }
     const float Mc = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)) + LM_C;
     float S = hw_exp2(-(Mc - x0)) * LM_SCALE;   // = fma(e, 256, 0): exact
     S = fmaf(hw_exp2(-(Mc - x1)), LM_SCALE, S);
     S = fmaf(hw_exp2(-(Mc - x2)), LM_SCALE, S);
     S = fmaf(hw_exp2(-(Mc - x3)), LM_SCALE, S);
     return (Mc - LM_C) + hw_log2(S);
-}
-
-// Two independent max* / lse4 as one packed stream (TDEC_LM_PK): the same IEEE
-// operations in the same order per element, so the same bits as jac / lse4,
-// with the subtraction, the fma and the final add (lse4: the shifts, scale,
-// fma chain and final add) issued as VOP3P pairs instead of two instructions
-// each (the transcendentals and maxima have no packed form).  Measured slower
-// (profiles/r03ad/: 149.1 vs 138.1 ms per 262 144 codewords, same bits): forming
-// the register pairs costs ~560 v_mov_b32 and the VOP3P hazards ~160 s_nop, more
-// than the paired operations save; off.
-#ifndef TDEC_LM_PK
-#define TDEC_LM_PK 0
-#endif
-__device__ __forceinline__ f2 jac2(f2 a, f2 b) {
-    const f2 d = a - b;
-    const f2 e = f2{hw_exp2(-(fabsf(d.x) + LM_C)), hw_exp2(-(fabsf(d.y) + LM_C))};
-    const f2 w = __builtin_elementwise_fma(e, f2{LM_SCALE, LM_SCALE}, f2{1.0f, 1.0f});
-    return f2{fmaxf(a.x, b.x), fmaxf(a.y, b.y)} + f2{hw_log2(w.x), hw_log2(w.y)};
-}
-__device__ __forceinline__ f2 lse4x2(f2 x0, f2 x1, f2 x2, f2 x3) {
-    const f2 Mc = f2{fmaxf(fmaxf(x0.x, x1.x), fmaxf(x2.x, x3.x)), fmaxf(fmaxf(x0.y, x1.y), fmaxf(x2.y, x3.y))} +
-                  f2{LM_C, LM_C};
-    const f2 K = f2{LM_SCALE, LM_SCALE};
-    const f2 d0 = Mc - x0, d1 = Mc - x1, d2 = Mc - x2, d3 = Mc - x3;
-    f2 S = f2{hw_exp2(-d0.x), hw_exp2(-d0.y)} * K;
-    S = __builtin_elementwise_fma(f2{hw_exp2(-d1.x), hw_exp2(-d1.y)}, K, S);
-    S = __builtin_elementwise_fma(f2{hw_exp2(-d2.x), hw_exp2(-d2.y)}, K, S);
-    S = __builtin_elementwise_fma(f2{hw_exp2(-d3.x), hw_exp2(-d3.y)}, K, S);
-    return (Mc - f2{LM_C, LM_C}) + f2{hw_log2(S.x), hw_log2(S.y)};
 }
 
 // The extrinsic's state groups: for input class c (0: inputs {0, 3}, 1: {1, 2},
@@ -287,14 +246,8 @@ template <int ALGO> __device__ __forceinline__ void alpha_step(float (&a)[NS], c
         const int p0 = t_prev_s(ns, 0), p1 = t_prev_s(ns, 2), q0 = t_prev_s(ns + 1, 0), q1 = t_prev_s(ns + 1, 2);
         const float x0 = a[p0] + pm_of(pm, p0, t_prev_i(ns, 0)), y0 = a[p1] + pm_of(pm, p1, t_prev_i(ns, 2));
         const float x1 = a[q0] + pm_of(pm, q0, t_prev_i(ns + 1, 0)), y1 = a[q1] + pm_of(pm, q1, t_prev_i(ns + 1, 2));
-        if constexpr (TDEC_LM_PK) {
-            const f2 r = jac2(f2{x0, x1}, f2{y0, y1});
-            na[ns] = r.x;
-            na[ns + 1] = r.y;
-        } else {
-            na[ns] = jac(x0, y0);
-            na[ns + 1] = jac(x1, y1);
-        }
+        na[ns] = jac(x0, y0);
+        na[ns + 1] = jac(x1, y1);
     }
     const float norm = na[0];
 #pragma unroll
@@ -330,14 +283,8 @@ template <int ALGO> __device__ __forceinline__ void beta_step(float (&b)[NS], co
     for (int s = 0; s < NS; s += 2) {
         const float x0 = b[t_next(s, 0)] + pm_of(pm, s, 0), y0 = b[t_next(s, 1)] + pm_of(pm, s, 1);
         const float x1 = b[t_next(s + 1, 0)] + pm_of(pm, s + 1, 0), y1 = b[t_next(s + 1, 1)] + pm_of(pm, s + 1, 1);
-        if constexpr (TDEC_LM_PK) {
-            const f2 r = jac2(f2{x0, x1}, f2{y0, y1});
-            nb[s] = r.x;
-            nb[s + 1] = r.y;
-        } else {
-            nb[s] = jac(x0, y0);
-            nb[s + 1] = jac(x1, y1);
-        }
+        nb[s] = jac(x0, y0);
+        nb[s + 1] = jac(x1, y1);
     }
     const float norm = nb[0];
 #pragma unroll
@@ -412,15 +359,8 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
                         const int st = LM_GROUPS.s[c][wy + h][i];
                         x[h][i] = a[st] + b1[t_next(st, c)];
                     }
-                if constexpr (TDEC_LM_PK) {
-                    const f2 r = lse4x2(f2{x[0][0], x[1][0]}, f2{x[0][1], x[1][1]}, f2{x[0][2], x[1][2]},
-                                        f2{x[0][3], x[1][3]});
-                    V[c][wy] = r.x;
-                    V[c][wy + 1] = r.y;
-                } else {
-                    V[c][wy] = lse4(x[0][0], x[0][1], x[0][2], x[0][3]);
-                    V[c][wy + 1] = lse4(x[1][0], x[1][1], x[1][2], x[1][3]);
-                }
+                V[c][wy] = lse4(x[0][0], x[0][1], x[0][2], x[0][3]);
+                V[c][wy + 1] = lse4(x[1][0], x[1][1], x[1][2], x[1][3]);
             }
         // app[inp] = +-U_c + X_c, X_c = lse4 over wy of (v(wy) + V[c][wy]): the two
         // inputs of a class share X_c (round 4; round 3 took one lse4 per input)
@@ -429,14 +369,8 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
         for (int c = 0; c < 2; ++c)
             X[c] = lse4(lm_v(g, 0) + V[c][0], lm_v(g, 1) + V[c][1], lm_v(g, 2) + V[c][2], lm_v(g, 3) + V[c][3]);
         const float app[4] = {g[0] + X[0], g[1] + X[1], -g[1] + X[1], -g[0] + X[0]};
-        if constexpr (TDEC_LM_PK) {
-            const f2 hi = jac2(f2{app[0], app[0]}, f2{app[1], app[2]}), lo = jac2(f2{app[2], app[1]}, f2{app[3], app[3]});
-            LpA = hi.x - lo.x;
-            LpB = hi.y - lo.y;
-        } else {
-            LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
-            LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
-        }
+        LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
+        LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
     }
     // bits -> nats (log-MAP), then the reference's f64 tail (:262-281)
     double x = ((ALGO ? (double)LpA * LM_LN2 : (double)LpA) - inA) * sf;
@@ -501,13 +435,10 @@ __device__ __forceinline__ double2 ld2(const lds_d2 *p) {
 __device__ __forceinline__ unsigned lds_addr(const lds_void *l) {
     return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
 }
-// TDEC_GLDS_SADDR: the staging DMAs address memory as a wave-uniform 64-bit base in
-// SGPRs plus a 32-bit per-lane byte offset (the instruction's saddr form) instead of
-// a 64-bit per-lane address: one VGPR per address instead of a pair (the paired
-// addresses of the backward passes' prologues were spilled).
-#ifndef TDEC_GLDS_SADDR
-#define TDEC_GLDS_SADDR 1
-#endif
+// The staging DMAs address memory as a wave-uniform 64-bit base in SGPRs plus a
+// 32-bit per-lane byte offset (the instruction's saddr form) instead of a 64-bit
+// per-lane address: one VGPR per address instead of a pair (the paired addresses
+// of the backward passes' prologues were spilled).
 __device__ __forceinline__ const void *uni_ptr(const void *p) {
     const unsigned long long u = (unsigned long long)p;
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
@@ -520,12 +451,6 @@ __device__ __forceinline__ void glds16s(const void *base, unsigned off, lds_void
 __device__ __forceinline__ void glds4s(const void *base, unsigned off, lds_void *l) {
     asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2" ::"s"(lds_addr(l)), "v"(off), "s"(uni_ptr(base))
                  : "memory");
-}
-__device__ __forceinline__ void glds16(const void *g, lds_void *l) {
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr(l)), "v"(g) : "memory");
-}
-__device__ __forceinline__ void glds4(const void *g, lds_void *l) {
-    asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_addr(l)), "v"(g) : "memory");
 }
 // s_waitcnt vmcnt(n) (lgkmcnt / expcnt left open): vector-memory operations
 // retire in issue order, so this retires everything but the last n issued.
@@ -565,13 +490,8 @@ struct TileIn {
         make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
-        if constexpr (TDEC_GLDS_SADDR) {
-            glds16s(X, (unsigned)(k * WAVE + lane) * 16u, st.v + j * WAVE);
-            glds16s(La, (wsrow(la_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
-        } else {
-            glds16(&at(X, k * WAVE + lane), st.v + j * WAVE);
-            glds16(&at(La, wsrow(la_idx[k], rs) + lane), st.l + j * WAVE);
-        }
+        glds16s(X, (unsigned)(k * WAVE + lane) * 16u, st.v + j * WAVE);
+        glds16s(La, (wsrow(la_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         Raw r;
@@ -606,18 +526,11 @@ struct TileInPre {
     }
     // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
-        const float *z = reinterpret_cast<const float *>(&at(Z, k * WAVE + lane));
         lds_f1 *dst = reinterpret_cast<lds_f1 *>(st.v + j * WAVE);
-        if constexpr (TDEC_GLDS_SADDR) {
-            const unsigned zo = (unsigned)(k * WAVE + lane) * 8u;
-            glds4s(Z, zo, dst);
-            glds4s(Z, zo + 4u, dst + WAVE);
-            glds16s(P, (wsrow(p_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
-        } else {
-            glds4(z, dst);
-            glds4(z + 1, dst + WAVE);
-            glds16(&at(P, wsrow(p_idx[k], rs) + lane), st.l + j * WAVE);
-        }
+        const unsigned zo = (unsigned)(k * WAVE + lane) * 8u;
+        glds4s(Z, zo, dst);
+        glds4s(Z, zo + 4u, dst + WAVE);
+        glds16s(P, (wsrow(p_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
         const lds_f1 *zp = reinterpret_cast<const lds_f1 *>(st.v + j * WAVE);
@@ -629,40 +542,13 @@ struct TileInPre {
     __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
 };
 
-// Workspace stores (extrinsic planes, checkpoints): nothing re-reads them before
-// L2 would have evicted them, so TDEC_NT_STORE marks them non-temporal.
-#ifndef TDEC_NT_STORE
-#define TDEC_NT_STORE 0
-#endif
-__device__ __forceinline__ void ws_store(double2 &dst, const double2 &v) {
-    if (TDEC_NT_STORE) __builtin_nontemporal_store((d2v){v.x, v.y}, reinterpret_cast<d2v *>(&dst));
-    else dst = v;
-}
-__device__ __forceinline__ void ws_store(float4 &dst, const float4 &v) {
-    if (TDEC_NT_STORE) __builtin_nontemporal_store((f4v){v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(&dst));
-    else dst = v;
-}
-
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
 // iteration) Le1 itself for the final decision (:529-530).
 // P1[k] is read by decoder 2 only as P1[perm[k']]: perm is not a permutation
 // (355 distinct values of 752 at N = 752), so rows outside its image are never
 // read and are not written (used[k] = 0): 53 % of the P1 stream at N = 752.
-#ifndef TDEC_P1_ALL
-#define TDEC_P1_ALL 0
-#endif
-// TDEC_SKIP_UNUSED: decoder 1 skips the extrinsic (and the alpha recompute that
-// only feeds it) at positions whose output no one reads; the store still goes
-// (to the sink row), so every path issues the same memory operations.
-#ifndef TDEC_SKIP_UNUSED
-#define TDEC_SKIP_UNUSED 1
-#endif
-#ifndef TDEC_SKIP_MID
-#define TDEC_SKIP_MID 0
-#endif
-#ifndef TDEC_SKIP_MID_LM
-#define TDEC_SKIP_MID_LM 0   // measured neutral (profiles/r03sk/ab3_lm*.log: 130.1-130.7 vs 130.0-130.5 ms)
-#endif
+// Decoder 1 also skips the extrinsic (and the alpha recompute that only feeds it)
+// at those positions before the last iteration (need()).
 // A discarded store goes to the wave's sink row (L2-resident) instead of being
 // skipped: every position issues the same stores, so the count of memory
 // operations between a load and its use is the same on every path and the
@@ -676,13 +562,13 @@ struct TileOutPre {
     // Whether anything reads the extrinsic at k: decoder 2 reads only the rows
     // in perm's image, so before the last iteration (Le null) the extrinsic of the
     // other 53 % (N = 752) is dead.  Wave-uniform (scalar load).
-    __device__ __forceinline__ bool need(int k) const { return TDEC_SKIP_UNUSED == 0 || TDEC_P1_ALL || Le || used[k]; }
+    __device__ __forceinline__ bool need(int k) const { return Le || used[k]; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
         // wave-uniform row selects (SGPR pairs), then the lane offset
-        double2 *rp = (TDEC_P1_ALL || used[k]) ? &at(P, wsrow(k, rs)) : sink;
+        double2 *rp = used[k] ? &at(P, wsrow(k, rs)) : sink;
         double2 *rl = Le ? &at(Le, wsrow(k, rs)) : sink;
-        ws_store(at(rp, (unsigned)lane), make_double2((double)lcA + a, (double)lcB + b));
-        ws_store(at(rl, (unsigned)lane), make_double2(a, b));
+        at(rp, (unsigned)lane) = make_double2((double)lcA + a, (double)lcB + b);
+        at(rl, (unsigned)lane) = make_double2(a, b);
     }
 };
 
@@ -692,7 +578,7 @@ struct TileOut {
     unsigned rs;
     __device__ __forceinline__ bool need(int) const { return true; }
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const {
-        ws_store(at(Le, wsrow(k, rs) + lane), make_double2(a, b));
+        at(Le, wsrow(k, rs) + lane) = make_double2(a, b);
     }
 };
 
@@ -768,19 +654,6 @@ __device__ __forceinline__ void load_vec(float (&x)[NS], const float4 *c, unsign
     }
 }
 
-template <bool ALPHA>
-__device__ __forceinline__ bool wave_all_equal(const float (&x)[NS], const float4 *c, unsigned cs, unsigned base,
-                                               int lane) {
-    bool eq = true;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float4 v = at(c, (base + q) * cs + lane);
-        eq &= (x[vec_elem<ALPHA>(q, 0)] == v.x) & (x[vec_elem<ALPHA>(q, 1)] == v.y) &
-              (x[vec_elem<ALPHA>(q, 2)] == v.z) & (x[vec_elem<ALPHA>(q, 3)] == v.w);
-    }
-    return __all(eq);
-}
-
 // This lane's vector equals the stored one (IEEE ==).  No short-circuit: with
 // `&&` the compiler issued the four loads one after another, each behind the
 // previous compare (four round trips per merge check instead of one; measured
@@ -809,8 +682,8 @@ template <bool ALPHA>
 __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base, int lane, const float (&x)[NS]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        ws_store(at(c, (base + q) * cs + lane), make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
-                                                            x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]));
+        at(c, (base + q) * cs + lane) = make_float4(x[vec_elem<ALPHA>(q, 0)], x[vec_elem<ALPHA>(q, 1)],
+                                                    x[vec_elem<ALPHA>(q, 2)], x[vec_elem<ALPHA>(q, 3)]);
 }
 
 // Window of the backward sweep fused with the extrinsic (:220-281): steps
@@ -826,11 +699,10 @@ __device__ __forceinline__ void store_vec(float4 *c, unsigned cs, unsigned base,
 // unconditional (the last window re-loads its own rows), so the number of
 // memory operations issued after them is the same on every path and the
 // compiler's wait counts stay exact.
-// B2 (CMP): `active` masks the stores of lanes that have merged.
-template <int ALGO, int W, bool RAG, bool CMP = false, class In, class Out>
+template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0, int len, Raw (&raw)[W],
                                             float (&an)[NS], float (&b)[NS], const float4 *ck, unsigned cs, int lane,
-                                            int N, double sf, bool active = true) {
+                                            int N, double sf) {
     // len = steps in this window (W except for a ragged top window when W does not divide N)
     float gw[W][8], lcA[W], lcB[W];
     double iAw[W], iBw[W];
@@ -849,27 +721,17 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
         for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(kn + j, N - 1) : kn + j);
         load_vec<true>(an, ck, cs, (kn / W) * 4, lane);
     }
-#ifndef TDEC_MID
-#define TDEC_MID 1
-#endif
     // alpha at the window midpoint (computed once) halves the recompute: positions
     // >= W/2 start from it, positions < W/2 from the checkpoint (log-MAP too since
     // its recursions combine branch pairs first: -5 % time, 68 instead of 270 B of
-    // scratch per lane)
-    constexpr int H = TDEC_MID ? W / 2 : 0;
+    // scratch per lane).  Skipping it where the positions it feeds are dead
+    // measured neutral (log-MAP) or slower (max-log, more spills): it always runs.
+    constexpr int H = W / 2;
     float am[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) am[s] = a0[s];
-    // the midpoint feeds only the extrinsics of positions >= H (log-MAP: one of
-    // its max*-heavy alpha steps per window of 2, skipped where decoder 1's
-    // output at k0 + 1 is dead)
-    bool needm = !(ALGO ? TDEC_SKIP_MID_LM : TDEC_SKIP_MID);
 #pragma unroll
-    for (int j = H; j < W; ++j) needm = needm || out.need(k0 + j);
-    if (needm) {
-#pragma unroll
-        for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
-    }
+    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
 #pragma unroll
     for (int j = W - 1; j >= 0; --j) {
         if (RAG && j >= len) continue;       // wave-uniform
@@ -887,7 +749,7 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
             for (int i = from; i < j; ++i) alpha_step<ALGO>(aj, gw[i]);
             extrinsic<ALGO>(aj, gw[j], b, iAw[j], iBw[j], sf, leA, leB);
         }
-        if (!CMP || active) out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
+        out.store(k0 + j, leA, leB, lcA[j], lcB[j]);
         beta_step<ALGO>(b, gw[j]);
     }
 }
@@ -915,53 +777,15 @@ __device__ __forceinline__ void back_window(const In &in, const Out &out, int k0
 // F1 of a SISO: alpha from a (zero) over all N steps, checkpoint every W steps,
 // inputs software-pipelined one group of FG steps ahead.  A deeper group than
 // W (FG = 8 at W = 4) measured no faster (round 2): F1's waits are already
-// covered, it is the backward windows that expose latency.
-#ifndef TDEC_FG
-#define TDEC_FG 4
-#endif
+// covered, it is the backward windows that expose latency.  log-MAP: one
+// checkpoint interval per group (its steps are ~10x larger, and the kernel's
+// instruction footprint, not load latency, is what costs).
+constexpr int FG_ML = 4, FG_LM = 2;
 // STORE = false: the recursion alone (log-MAP's F1, whose checkpoints F2 would
-// overwrite almost everywhere: see TDEC_LM_F1_PLAIN).
-// CKI: checkpoint interval when it differs from the group interval W (siso8 with
-// TDEC_CK16: groups of 8 steps, a checkpoint at every other group).
-template <int ALGO, int W, bool RAG, bool STORE = true, int CKI = W, class In>
+// overwrite almost everywhere, see siso<>).
+template <int ALGO, int W, bool RAG, bool STORE = true, class In>
 __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigned cs, int lane, float (&a)[NS]) {
-    static_assert(CKI % W == 0, "checkpoint interval: a multiple of the group interval");
-    // log-MAP: one checkpoint interval per group (its steps are ~10x larger, and
-    // the kernel's instruction footprint, not load latency, is what costs)
-#ifndef TDEC_FG_LM
-#define TDEC_FG_LM 2
-#endif
-    // TDEC_F1_ROLL = R > 0 (max-log): a rolling prefetch instead of groups: step
-    // j's input slot is refilled with step j + R's input right after its branch
-    // metrics are formed, so every load has R steps of work to land (the grouped
-    // form gives it only the group's alpha steps) and only one step's metrics
-    // are held.
-#ifndef TDEC_F1_ROLL
-#define TDEC_F1_ROLL 0
-#endif
-    if constexpr (ALGO == 0 && TDEC_F1_ROLL > 0) {
-        constexpr int R = TDEC_F1_ROLL > 0 ? TDEC_F1_ROLL : W;
-        static_assert(R % W == 0, "TDEC_F1_ROLL must be a multiple of W");
-        const bool tail = RAG || N % R != 0;
-        Raw raw[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) raw[j] = in.load(tail ? min(j, N - 1) : j);
-        for (int k0 = 0; k0 < N; k0 += R) {
-            const bool more = k0 + R < N;
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                if (tail && k0 + j >= N) continue;   // wave-uniform
-                float g[8];
-                double iA, iB;
-                in.template gamma<ALGO>(raw[j], g, iA, iB);
-                if (more) raw[j] = in.load(tail ? min(k0 + R + j, N - 1) : k0 + R + j);
-                if (STORE && j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
-                alpha_step<ALGO>(a, g);
-            }
-        }
-        return;
-    }
-    constexpr int FGW = ALGO ? TDEC_FG_LM : TDEC_FG;
+    constexpr int FGW = ALGO ? FG_LM : FG_ML;
     constexpr int FG = FGW > W ? FGW : W;   // a multiple of W
     static_assert(FG % W == 0, "FG must be a multiple of W");
     // steps past N exist only when W does not divide N (RAG) or FG > W
@@ -984,8 +808,7 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
 #pragma unroll
         for (int j = 0; j < FG; ++j) {
             if (tail && k0 + j >= N) continue;
-            if (STORE && j % W == 0 && (CKI == W || (k0 + j) % CKI == 0))
-                store_vec<true>(ck, cs, ((k0 + j) / CKI) * 4, lane, a);
+            if (STORE && j % W == 0) store_vec<true>(ck, cs, ((k0 + j) / W) * 4, lane, a);
             alpha_step<ALGO>(a, g[j]);
         }
     }
@@ -997,9 +820,12 @@ __device__ __forceinline__ void f1_pass(const In &in, int N, float4 *ck, unsigne
 // lane merges after 83 % (F2) / 89 % (B2) of N, median lane 27 %; max-log: 29 %),
 // so the provisional extrinsic of B1 is recomputed almost everywhere anyway:
 // one beta-only pass + one full pass does less work than two extrinsic passes.
+// log-MAP's F1 likewise: alpha1 without checkpoints, then F2 over the whole block
+// storing every checkpoint (no merge test): fewer bytes (F2 would rewrite 83 % of
+// the checkpoints after reading them for the test) for 17 % more F2 steps.
 template <int ALGO, bool RAG, class In>
 __device__ __forceinline__ void b1_pass(const In &in, int N, float (&b)[NS]) {
-    constexpr int FG = ALGO ? TDEC_FG_LM : TDEC_FG;
+    constexpr int FG = ALGO ? FG_LM : FG_ML;
     Raw raw[FG];
     // groups [k1 - FG, k1) from the top; the lowest may be short (wave-uniform guards)
 #pragma unroll
@@ -1021,37 +847,18 @@ __device__ __forceinline__ void b1_pass(const In &in, int N, float (&b)[NS]) {
             if (k1 - FG + j >= 0) beta_step<ALGO>(b, g[j]);
     }
 }
-#ifndef TDEC_LM_B1_PLAIN
-#define TDEC_LM_B1_PLAIN 1
-#endif
-// log-MAP's F1 likewise: alpha1 without checkpoints, then F2 over the whole block
-// storing every checkpoint (no merge test): fewer bytes (F2 would rewrite 83 % of
-// the checkpoints after reading them for the test) for 17 % more F2 steps.
-#ifndef TDEC_LM_F1_PLAIN
-#define TDEC_LM_F1_PLAIN 1
-#endif
 
-#ifndef TDEC_UNMASK_ML
-#define TDEC_UNMASK_ML 0
-#endif
-#ifndef TDEC_UNMASK_LM
-#define TDEC_UNMASK_LM 1
-#endif
-#ifndef TDEC_LANE_MERGE
-#define TDEC_LANE_MERGE 1
-#endif
 constexpr int RING = 16;   // beta1 kept at RING window starts 16 steps apart: the top 256 steps (merge: median 40, max 122)
 __host__ __device__ constexpr int rstep_of(int w) { return w >= 16 ? 1 : 16 / w; }
 
-// Issue priority (TDEC_PRIO, see progress_prio below): 1 = by progress through
-// the tile; 2 = by pass (forward passes 3, backward 1); 3 = both (first half of
-// the tile: forward 3, backward 2; second half: 1, 0); 4 = against the other
-// wave of the same SIMD: each wave publishes its progress (half SISOs since the
-// launch) in a per-SIMD table indexed by HW_ID / XCC_ID and issues first while
-// it is behind.
-#ifndef TDEC_PRIO
-#define TDEC_PRIO 4
-#endif
+// Issue priority of the throughput decoder (max-log): each wave publishes its
+// progress (half SISOs since the launch) in a per-SIMD table indexed by HW_ID /
+// XCC_ID and issues first while it is behind the other wave of its SIMD (the two
+// otherwise issue oldest first, and with one tile each the younger runs its last
+// ~3 ms alone at the one-wave rate: configs[1] 10.6 -> 9.8-9.9 ms per 102 400
+// codewords, profiles/r03t/, r03z/).  Policies by tile progress or by pass, a finer
+// comparison (4 units per SISO) and the same policy in the log-MAP decoder
+// measured no better (profiles/r03x/, r03ab/, r03ac/).
 __device__ __forceinline__ void set_prio(int v) {
     switch (v) {
     case 3: __builtin_amdgcn_s_setprio(3); break;
@@ -1061,8 +868,7 @@ __device__ __forceinline__ void set_prio(int v) {
     }
 }
 struct Prio {
-    int hi = 3;           // TDEC_PRIO 3: this SISO's forward level (3 or 1 by tile half)
-    int *tab = nullptr;   // TDEC_PRIO 4: this SIMD's 16 progress slots (by wave id), or null
+    int *tab = nullptr;   // this SIMD's 16 progress slots (by wave id), or null
     int me = 0;           // this wave's slot
     int prog = 0;         // half SISOs completed before this SISO
 };
@@ -1076,108 +882,49 @@ __device__ __forceinline__ void mate_prio(const Prio &pr, int v) {
     for (int l = 0; l < 16; ++l) mate = max(mate, __builtin_amdgcn_readlane(x, l));
     set_prio(mate == 0 ? 2 : (v + 1 < mate ? 3 : (v + 1 > mate ? 1 : 2)));
 }
-// TDEC_PRIO_FINE: policy 4 also compares halfway through B1 and at B2's start
-// (4 progress units per SISO instead of 2).  Measured no better: configs[1]
-// 9.93-9.95 vs 9.91-9.95 ms, 1 M codewords 247.9 vs 243.6 ms (profiles/r03ab/).
-#ifndef TDEC_PRIO_FINE
-#define TDEC_PRIO_FINE 0
-#endif
-constexpr int PRIO_UNITS = TDEC_PRIO_FINE ? 4 : 2;
-__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr, int unit = -1) {
-    if constexpr (TDEC_PRIO == 2) set_prio(forward ? 3 : 1);
-    if constexpr (TDEC_PRIO == 3) set_prio(forward ? pr.hi : pr.hi - 1);
-    if constexpr (TDEC_PRIO == 4) {
-        if (pr.tab) mate_prio(pr, pr.prog + (unit >= 0 ? unit : (forward ? 0 : 1)));
-    }
+constexpr int PRIO_UNITS = 2;   // progress units per SISO (forward half, backward half)
+__device__ __forceinline__ void phase_prio(bool forward, const Prio &pr) {
+    if (pr.tab) mate_prio(pr, pr.prog + (forward ? 0 : 1));
 }
 
-// TDEC_PRIO_LM: policy 4 in the log-MAP decoder too.  Measured no different at
-// 1 M codewords (533.5 vs 533.7, 535.3 vs 536.3 ms: profiles/r03ac/), so off.
-#ifndef TDEC_PRIO_LM
-#define TDEC_PRIO_LM 0
-#endif
+// The SISO with checkpoints every W steps (the row SISO, the fused demap-decode
+// kernel and the log-MAP throughput decoder; max-log's throughput decoder runs
+// siso8 below).
 template <int ALGO, int W, bool RAG, class In, class Out>
 __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane,
-                     double sf, const Prio &pr = Prio{}) {
-    if (TDEC_PRIO_LM) phase_prio(true, pr);
+                     double sf) {
     const int top = RAG ? ((N - 1) / W) * W : N - W;   // start of the (possibly short) top window
     constexpr int RSTEP = rstep_of(W);
     Raw raw[W];
-    float a[NS];
+    float a[NS], b[NS], an[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) a[s] = 0.0f;
-    constexpr bool UNMASK = ALGO ? TDEC_UNMASK_LM : TDEC_UNMASK_ML;
-    bool merged = false;
-    if constexpr (ALGO != 0 && TDEC_LM_F1_PLAIN) {
+    for (int s = 0; s < NS; ++s) a[s] = b[s] = 0.0f;
+    if constexpr (ALGO != 0) {
         f1_pass<ALGO, W, RAG, false>(in, N, ck, cs, lane, a);   // a = alpha1[N] = alpha2[0]
         f1_pass<ALGO, W, RAG, true>(in, N, ck, cs, lane, a);    // alpha2, every checkpoint
-    } else {
+        b1_pass<ALGO, RAG>(in, N, b);                           // b = beta1[0] = beta2[N]
+#pragma unroll
+        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
+        load_vec<true>(an, ck, cs, (top / W) * 4, lane);
+        for (int k0 = top; k0 >= 0; k0 -= W)
+            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
+        return;
+    }
     // F1 (inputs software-pipelined one group of FG steps ahead)
     f1_pass<ALGO, W, RAG>(in, N, ck, cs, lane, a);
     // F2 until merged (a = alpha1[N] = alpha2[0]).  Per lane: once alpha2 ==
     // alpha1 at a checkpoint, every later checkpoint already holds alpha2, so
     // the lane stops loading and storing (masked lanes move no bytes); the
-    // wave runs until every lane has merged.
+    // wave runs until every lane has merged.  (The unmasked form -- every lane
+    // loads, merged lanes only skip stores -- measured slower for max-log: 66.7 vs
+    // 64.6 ms per 262 144 codewords, round 2.)
 #pragma unroll
     for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(j, N - 1) : j);
-    // Two forms of the partial passes F2 / B2 (bit-identical):
-    //  masked:   a merged lane issues no loads or stores (fewer bytes; the branch
-    //            around them makes the compiler wait for every outstanding load)
-    //  unmasked: every lane loads (the inputs and the next compare vector one
-    //            group / window ahead, with exact wait counts); merged lanes
-    //            only skip their stores.
-    // Measured (round 2, 262 144 codewords): max-log masked 64.6 ms vs unmasked
-    // 66.7 (HBM-bound: bytes win), log-MAP masked 399.1 vs unmasked 393.0 ms.
-    if (TDEC_LANE_MERGE && !UNMASK) {
-        for (int k0 = 0; k0 < N; k0 += W) {
-            if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / W) * 4, lane);
-            if (__all(merged)) break;
-            if (!merged) {
-                float g[W][8];
-#pragma unroll
-                for (int j = 0; j < W; ++j) {
-                    double iA, iB;
-                    in.template gamma<ALGO>(raw[j], g[j], iA, iB);
-                }
-                if (k0 + W < N) {
-#pragma unroll
-                    for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(k0 + W + j, N - 1) : k0 + W + j);
-                }
-                store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
-#pragma unroll
-                for (int j = 0; j < W; ++j)
-                    if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
-            }
-        }
-    } else if (TDEC_LANE_MERGE) {
-        // The checkpoint each group compares against is loaded one group ahead,
-        // with the inputs, before the group's checkpoint store; all loads are
-        // unconditional, so no branch makes the compiler wait for them early.
-        // (Running F1 as pass 0 of this loop, one copy of the code, measured no
-        // faster: 385.3 vs 381.1 ms per 262 144 log-MAP codewords.)
-        float c[NS];
-        load_vec<true>(c, ck, cs, 0, lane);
-        for (int k0 = 0; k0 < N; k0 += W) {
-            if (!merged) merged = vec_equal(a, c);
-            if (__all(merged)) break;
-            float g[W][8];
-#pragma unroll
-            for (int j = 0; j < W; ++j) {
-                double iA, iB;
-                in.template gamma<ALGO>(raw[j], g[j], iA, iB);
-            }
-            const int kn = k0 + W < N ? k0 + W : k0;
-#pragma unroll
-            for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(kn + j, N - 1) : kn + j);
-            load_vec<true>(c, ck, cs, (kn / W) * 4, lane);
-            if (!merged) store_vec<true>(ck, cs, (k0 / W) * 4, lane, a);
-#pragma unroll
-            for (int j = 0; j < W; ++j)
-                if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
-        }
-    } else {
-        for (int k0 = 0; k0 < N; k0 += W) {
-            if (wave_all_equal<true>(a, ck, cs, (k0 / W) * 4, lane)) break;
+    bool merged = false;
+    for (int k0 = 0; k0 < N; k0 += W) {
+        if (!merged) merged = lane_equal<true>(a, ck, cs, (k0 / W) * 4, lane);
+        if (__all(merged)) break;
+        if (!merged) {
             float g[W][8];
 #pragma unroll
             for (int j = 0; j < W; ++j) {
@@ -1194,25 +941,11 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
                 if (!RAG || k0 + j < N) alpha_step<ALGO>(a, g[j]);
         }
     }
-    }   // F1 + F2
     // B1 fused with the provisional extrinsic, then B2 until merged (b =
     // beta1[0] = beta2[N]); per lane as F2: below its merge point a lane's
     // provisional extrinsics are exact, it stops there.  One copy of the window
     // code serves both passes (the pass loop is not unrolled: the kernels'
     // instruction footprint, see siso8).
-    float b[NS], an[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) b[s] = 0.0f;
-    if constexpr (ALGO != 0 && TDEC_LM_B1_PLAIN) {
-        if (TDEC_PRIO_LM) phase_prio(false, pr);
-        b1_pass<ALGO, RAG>(in, N, b);   // b = beta1[0] = beta2[N]
-#pragma unroll
-        for (int j = 0; j < W; ++j) raw[j] = in.load(RAG ? min(top + j, N - 1) : top + j);
-        load_vec<true>(an, ck, cs, (top / W) * 4, lane);
-        for (int k0 = top; k0 >= 0; k0 -= W)
-            back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
-        return;
-    }
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
@@ -1225,23 +958,13 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
             if (pass == 0) {
                 if (keep) store_vec<false>(ring, cs, r / RSTEP * 4, lane, b);   // beta1 entering
             } else if (keep) {
-                if (TDEC_LANE_MERGE) {
-                    float rv[NS];
-                    load_vec<false>(rv, ring, cs, r / RSTEP * 4, lane);
-                    if (!merged) merged = vec_equal(b, rv);
-                    if (__all(merged)) break;
-                } else if (wave_all_equal<false>(b, ring, cs, r / RSTEP * 4, lane)) {
-                    break;
-                }
+                float rv[NS];
+                load_vec<false>(rv, ring, cs, r / RSTEP * 4, lane);
+                if (!merged) merged = vec_equal(b, rv);
+                if (__all(merged)) break;
             }
-            if (UNMASK) {
-                // a merged lane keeps stepping (its later values equal beta1's) but
-                // stores nothing
-                back_window<ALGO, W, RAG, true>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N,
-                                                sf, !merged);
-            } else if (!merged) {
+            if (!merged)
                 back_window<ALGO, W, RAG>(in, out, k0, RAG ? min(W, N - k0) : W, raw, an, b, ck, cs, lane, N, sf);
-            }
         }
     }
 }
@@ -1259,30 +982,20 @@ __device__ void siso(const In &in, const Out &out, int N, float4 *ck, float4 *ri
 
 // Positions kb+3 .. kb of a half window (kb+len-1 .. kb if ragged), alpha[kb]
 // given, midpoint recompute as back_window.
-// MID: am (alpha[kb+2]) is given by the caller instead of recomputed from a0.
-template <int ALGO, bool RAG, bool MID = false, class Out>
+template <int ALGO, bool RAG, class Out>
 __device__ __forceinline__ void window_half(const Out &out, int kb, int len, const float (&a0)[NS],
                                             const float (&gw)[4][8], const double (&iAw)[4], const double (&iBw)[4],
-                                            const float (&lcA)[4], const float (&lcB)[4], float (&b)[NS], double sf,
-                                            const float *mid = nullptr) {
+                                            const float (&lcA)[4], const float (&lcB)[4], float (&b)[NS], double sf) {
     constexpr int H = 2;
     float am[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) am[s] = MID ? mid[s] : a0[s];
-    if constexpr (!MID) {
-        // the midpoint feeds only the extrinsics of positions 2 and 3
-        if (!TDEC_SKIP_MID || out.need(kb + 2) || out.need(kb + 3)) {
+    for (int s = 0; s < NS; ++s) am[s] = a0[s];
 #pragma unroll
-            for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
-        }
-    }
+    for (int i = 0; i < H; ++i) alpha_step<ALGO>(am, gw[i]);
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
         if (RAG && j >= len) continue;       // wave-uniform
-#ifndef TDEC_HALF_SB
-#define TDEC_HALF_SB 1
-#endif
-        if (TDEC_HALF_SB) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
         const int from = j >= H ? H : 0;
         double leA = 0.0, leB = 0.0;
         if (out.need(kb + j)) {
@@ -1317,10 +1030,7 @@ __device__ __forceinline__ void window_half(const Out &out, int kb, int len, con
 // registers across the top half.
 __device__ __forceinline__ void ck_stage(const float4 *ck, unsigned cs, unsigned base, int lane, lds_f4 *slot) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if constexpr (TDEC_GLDS_SADDR) glds16s(ck, ((base + q) * cs + lane) * 16u, slot + q * WAVE);
-        else glds16(&at(ck, (base + q) * cs + lane), slot + q * WAVE);
-    }
+    for (int q = 0; q < 4; ++q) glds16s(ck, ((base + q) * cs + lane) * 16u, slot + q * WAVE);
 }
 __device__ __forceinline__ void ck_read(const lds_f4 *slot, int lane, float (&x)[NS]) {
 #pragma unroll
@@ -1353,15 +1063,10 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
 #pragma unroll
     for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
     in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
-    // TDEC_KEEP_MID: alpha[k0+2], passed on the way to alpha[k0+4], is kept for
-    // the bottom half's midpoint instead of being recomputed there.  Measured
-    // slower (profiles/r03w/: 250.9 vs 244.2 ms per 1 M codewords, configs[1]
-    // 14.0 vs 10.4 ms): the 16 registers it holds across the top half cost more
-    // than the two alpha steps it saves.
-#ifndef TDEC_KEEP_MID
-#define TDEC_KEEP_MID 0
-#endif
-    float a2[NS];
+    // (Keeping alpha[k0+2], passed on the way to alpha[k0+4], for the bottom half's
+    // midpoint measured slower: profiles/r03w/, 250.9 vs 244.2 ms per 1 M codewords,
+    // configs[1] 14.0 vs 10.4 ms -- the 16 registers it holds across the top half
+    // cost more than the two alpha steps it saves.)
     if (!RAG || lenT > 0) {
         float a4[NS];    // alpha[k0+4]: 4 steps from the checkpoint over the staged bottom half
         ck_read(st.ck, lane, a4);
@@ -1371,10 +1076,6 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             double x, y;
             in.template gamma<ALGO>(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
-            if (TDEC_KEEP_MID && i == 1) {
-#pragma unroll
-                for (int s = 0; s < NS; ++s) a2[s] = a4[s];
-            }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
@@ -1398,110 +1099,14 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     // needed at once by the bottom half, so the wait costs nothing.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
-    if (TDEC_KEEP_MID && (!RAG || lenT > 0))
-        window_half<ALGO, RAG, true>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf, a2);
-    else
-        window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
-}
-
-// TDEC_CK16 (build variant): alpha checkpoints every 16 steps
-// instead of 8 (half the checkpoint bytes: 64 B per lane per 16 steps written by
-// F1/F2 and read back by B1/B2), the backward sweep still in windows of 8.  The
-// slot then holds alpha[16 floor(k0 / 16)]: an even window (k0 % 16 == 0) reads
-// it as before; an odd one first climbs 8 steps over the NEXT window's inputs
-// (its bottom half staged into sn and its top half loaded into rt at this
-// window's start, so nothing is read twice) to alpha[k0], and the slot keeps
-// alpha[k0 - 8], which is the next window's checkpoint.  alpha[k0] is held in
-// registers across the top half (the register cost TDEC_KEEP_MID measured), the
-// climb waits for loads issued at the window's start, and each odd window does
-// 8 more gammas and alpha steps.  Same f32 / f64 operations: bit-identical.
-#ifndef TDEC_CK16
-#define TDEC_CK16 0
-#endif
-template <int ALGO, bool RAG, class In, class Out>
-__device__ __forceinline__ void back_window16(const In &in, const Out &out, int k0, int len, Raw (&rt)[4],
-                                              const LdsStage &st, const LdsStage &sn,
-                                              float (&b)[NS], const float4 *ck, unsigned cs, int lane, int N,
-                                              double sf) {
-    const int lenT = RAG ? (len > 4 ? len - 4 : 0) : 4;
-    const int lenB = RAG ? (len < 4 ? len : 4) : 4;
-    const int kn = k0 >= 8 ? k0 - 8 : 0;   // the next window
-    const bool odd = (k0 & 8) != 0;       // wave-uniform
-    float gw[4][8], lcA[4], lcB[4];
-    double iAw[4], iBw[4];
-    if (!RAG || lenT > 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            in.template gamma<ALGO>(rt[j], gw[j], iAw[j], iBw[j]);
-            lcA[j] = rt[j].v.x;
-            lcB[j] = rt[j].v.y;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
-    float a0[NS];
-    if (odd) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rt[j] = in.load(kn + 4 + j);
-        wait_vm<0>();   // sn (this window's DMA) and rt: the climb reads both now
-        ck_read(st.ck, lane, a0);   // alpha[k0 - 8]
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float g[8];
-            double x, y;
-            in.template gamma<ALGO>(in.staged(sn, i), g, x, y);
-            alpha_step<ALGO>(a0, g);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float g[8];
-            double x, y;
-            in.template gamma<ALGO>(rt[i], g, x, y);
-            alpha_step<ALGO>(a0, g);
-        }
-    } else {
-        in.wait_staged();   // st and the slot's DMA have landed (sn may still be in flight)
-        ck_read(st.ck, lane, a0);
-        // the slot's last read has returned before the DMA that overwrites it (back_window8)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        ck_stage(ck, cs, (kn / 16) * 4, lane, st.ck);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
-    }
-    if (!RAG || lenT > 0) {
-        float a4[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            a4[s] = a0[s];
-            asm volatile("" : "+v"(a4[s]));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float g[8];
-            double x, y;
-            in.template gamma<ALGO>(in.staged(st, i), g, x, y);
-            alpha_step<ALGO>(a4, g);
-        }
-        window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const Raw r = in.staged(st, j);
-        in.template gamma<ALGO>(r, gw[j], iAw[j], iBw[j]);
-        lcA[j] = r.v.x;
-        lcB[j] = r.v.y;
-    }
     window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
-// beta1 kept at every RSTEP8-th window start: 2 = the same 16-step grid over the
-// top 256 steps as siso<>; 1 (build variant) = an 8-step grid over the top 128
-// steps, so B2 stops up to 8 steps earlier for the same ring writes, but lanes
-// that merge below the top 128 steps run B2 to the end.
-#ifndef TDEC_RSTEP8
-#define TDEC_RSTEP8 2
-#endif
-constexpr int RSTEP8 = TDEC_RSTEP8;
+// beta1 kept at every 2nd window start: the same 16-step grid over the top 256
+// steps as siso<>.  (An 8-step grid over the top 128 steps -- B2 stops up to 8 steps
+// earlier for the same ring writes -- measured neutral at N = 212 and slower at
+// 752, where lanes merging below the top 128 steps run B2 to the end.)
+constexpr int RSTEP8 = 2;
 
 // TDEC_PASS_TIMING (measurement build): per-pass shader-clock cycles summed
 // over all waves (s_memtime, one vector atomic from lane 0 per pass), printed
@@ -1531,22 +1136,19 @@ __device__ __forceinline__ void pass_mark(unsigned long long &, int) {}
 __device__ __forceinline__ void merge_mark(int, int, int) {}
 #endif
 
-#ifndef TDEC_LAUNDER_LANE
-#define TDEC_LAUNDER_LANE 1
-#endif
 template <int ALGO, bool RAG, class In, class Out>
 __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *ring, unsigned cs, int lane, double sf,
                       const LdsStage &lb, const LdsStage &lb1, const Prio &pr = Prio{}) {
     unsigned long long tpass = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
     phase_prio(true, pr);
-    constexpr int G = 4, WS = 8, CK = TDEC_CK16 ? 16 : 8;   // window step, checkpoint interval
+    constexpr int G = 4, WS = 8, CK = 8;   // group, window step, checkpoint interval
     const int top = RAG ? ((N - 1) / WS) * WS : N - WS;
     Raw raw[G];
     float a[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) a[s] = 0.0f;
     // F1: inputs pipelined one group of FG steps ahead, checkpoint every 8
-    f1_pass<ALGO, WS, RAG, true, CK>(in, N, ck, cs, lane, a);
+    f1_pass<ALGO, WS, RAG, true>(in, N, ck, cs, lane, a);
     pass_mark(tpass, 0);
     // F2 until merged with F1 at a checkpoint.  (Measured alternative, round 2:
     // the next checkpoint prefetched one interval ahead with unmasked input
@@ -1592,29 +1194,21 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
     float b[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) b[s] = 0.0f;
-    // TDEC_B_ONECOPY: B1 and B2 share one copy of the window code (the pass
-    // loop is not unrolled), halving the backward sweep's instruction footprint:
-    // the kernel shrinks from 15.2 k to 9.6 k instructions and decodes 1.5 %
-    // faster (62.6 -> 61.7 ms per 262 144 codewords, same bits): the waves of a
-    // CU run different passes at once and share its instruction cache.
-#ifndef TDEC_B_ONECOPY
-#define TDEC_B_ONECOPY 1
-#endif
-#if TDEC_B_ONECOPY
+    // B1 and B2 share one copy of the window code (the pass loop is not
+    // unrolled), halving the backward sweep's instruction footprint: the kernel
+    // shrinks from 15.2 k to 9.6 k instructions and decodes 1.5 % faster (62.6 ->
+    // 61.7 ms per 262 144 codewords, same bits): the waves of a CU run different
+    // passes at once and share its instruction cache.
 #pragma unroll 1
-#else
-#pragma unroll
-#endif
     for (int pass = 0; pass < 2; ++pass) {
-        if (TDEC_PRIO_FINE && pass == 1) phase_prio(false, pr, 3);
-        // TDEC_LAUNDER_LANE: the lane index goes through an empty asm here, so the
-        // per-lane addresses of this prologue are formed from it again (a shift and
-        // an add each) instead of hoisted out of the tile's loops and spilled: the
-        // spilled ones came back through scratch loads, each followed by a full
-        // vmcnt(0) wait ahead of the DMA that needed it.
+        // The lane index goes through an empty asm here, so the per-lane addresses
+        // of this prologue are formed from it again (a shift and an add each)
+        // instead of hoisted out of the tile's loops and spilled: the spilled ones
+        // came back through scratch loads, each followed by a full vmcnt(0) wait
+        // ahead of the DMA that needed it.
         In inp = in;
         int lanep = lane;
-        if constexpr (TDEC_LAUNDER_LANE) asm volatile("" : "+v"(inp.lane), "+v"(lanep));
+        asm volatile("" : "+v"(inp.lane), "+v"(lanep));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             raw[j] = inp.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
@@ -1626,7 +1220,6 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         for (int k0 = top; k0 >= 0; k0 -= WS) {
             const int r = (top - k0) / WS;
             const bool keep = r % RSTEP8 == 0 && r < RING * RSTEP8;
-            if (TDEC_PRIO_FINE && pass == 0 && r == top / (2 * WS)) phase_prio(false, pr, 2);
             if (pass == 0 && keep) store_vec<false>(ring, cs, r / RSTEP8 * 4, lane, b);   // beta1 entering
             if (pass == 1 && keep) {
                 if (!merged) {
@@ -1640,12 +1233,8 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
             }
             if (!merged) {
                 const bool odd = r & 1;
-                if constexpr (TDEC_CK16)
-                    back_window16<ALGO, RAG>(in, out, k0, RAG ? min(WS, N - k0) : WS, raw, odd ? lb1 : lb,
-                                             odd ? lb : lb1, b, ck, cs, lane, N, sf);
-                else
-                    back_window8<ALGO, RAG>(in, out, k0, RAG ? min(WS, N - k0) : WS, raw, odd ? lb1 : lb,
-                                            odd ? lb : lb1, b, ck, cs, lane, N, sf);
+                back_window8<ALGO, RAG>(in, out, k0, RAG ? min(WS, N - k0) : WS, raw, odd ? lb1 : lb,
+                                        odd ? lb : lb1, b, ck, cs, lane, N, sf);
             }
         }
         pass_mark(tpass, 2 + pass);
@@ -1662,30 +1251,18 @@ constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
 // wave slots (one round, e.g. configs[1]: 1 600 tiles for 2 048 slots) four-wave
 // blocks leave some CUs with 8 waves and others with 4, and the launch lasts as
 // long as the fullest CU (a CU's memory pipeline, not its SIMDs, is what a tile
-// waits on: profiles/r03p/c1_batch_sweep.txt).
-#ifndef TDEC_DEC_WAVES
-#define TDEC_DEC_WAVES 4
-#endif
-constexpr int DEC_WAVES = TDEC_DEC_WAVES;
+// waits on: profiles/r03p/c1_batch_sweep.txt; one- and four-wave blocks measured equal).
+constexpr int DEC_WAVES = 4;
 constexpr int DEC_BLOCK = DEC_WAVES * WAVE;
-#ifndef TDEC_WIN
-#define TDEC_WIN 4
-#endif
-constexpr int WIN = TDEC_WIN;            // alpha checkpoint interval of the row SISO (k_siso_batch)
-#ifndef TDEC_WIN_ML
-#define TDEC_WIN_ML 8
-#endif
+constexpr int WIN = 4;                   // alpha checkpoint interval of the row SISO (k_siso_batch)
 // max-log checkpoint interval of k_turbo_decode: 8 (siso8: LDS-DMA staged half
-// windows, bit-identical) or 4 (siso<>, build variant TDEC_WIN_ML=4).  8 moves
-// 13 % fewer bytes per codeword; it was slower (round 1: 73.7 vs 69.8 ms per
-// 262 144 codewords) until its loads were issued a half window or more ahead
-// with exact wait counts (inline-asm LDS DMA, checkpoint slot in LDS, 32-bit LDS
-// pointers): round 2, 62.4 vs 65.0 ms (tools/ab.py, same bits).
-constexpr int WIN_ML = TDEC_WIN_ML;
-#ifndef TDEC_WIN_LM
-#define TDEC_WIN_LM 2
-#endif
-constexpr int WIN_LM = TDEC_WIN_LM;      // log-MAP turbo decoder's checkpoint interval
+// windows, bit-identical to siso<> at 4).  8 moves 13 % fewer bytes per codeword;
+// it was slower (round 1: 73.7 vs 69.8 ms per 262 144 codewords) until its loads
+// were issued a half window or more ahead with exact wait counts (inline-asm LDS
+// DMA, checkpoint slot in LDS, 32-bit LDS pointers): round 2, 62.4 vs 65.0 ms
+// (tools/ab.py, same bits).  16 measured slower.
+constexpr int WIN_ML = 8;
+constexpr int WIN_LM = 2;                // log-MAP turbo decoder's checkpoint interval
 __host__ __device__ constexpr int win_of(int algo) { return algo ? WIN_LM : WIN_ML; }
 constexpr int LDS_STAGE1 = DEC_WAVES * 4 * WAVE;   // float4 / double2 entries of one staging buffer of a block
 constexpr int LDS_STAGE = LDS_STAGE1 * 2;   // double-buffered (siso8)
@@ -1694,12 +1271,11 @@ constexpr int LDS_STAGE = LDS_STAGE1 * 2;   // double-buffered (siso8)
 // bit-packing words then live in the wave's own first staging slice (idle
 // between tiles) instead of a separate array that would not fit.
 constexpr int LDS_LV = LDS_STAGE + DEC_WAVES * 4 * WAVE;
-constexpr int EPI_STRIDE_ML = TDEC_WIN_ML == 8 ? 4 * WAVE * 4 : 2 * WAVE;   // uint32 words between waves' epi areas
+constexpr int EPI_STRIDE_ML = 4 * WAVE * 4;   // uint32 words between waves' epi areas
 
 // The SISO of the tile decoder: siso8 (LDS-staged, checkpoints every 8) for
 // max-log when the kernel provides the staging LDS (STAGED), else siso<> with
 // checkpoints every 4 (max-log, the fused demap-decode kernel) or WIN_LM.
-constexpr bool STAGED_ML = WIN_ML == 8;
 __host__ __device__ constexpr int win_unstaged(int algo) { return algo ? WIN_LM : 4; }
 // A handle's checkpoint rows are sized for the densest interval among the kernels
 // that can run for its algorithm: the row SISO (WIN), the tile decoder
@@ -1717,7 +1293,7 @@ __device__ __forceinline__ void run_siso(const In &in, const Out &out, int N, fl
         siso8<ALGO, RAG>(in, out, N, ck, ring, cs, lane, sf, LdsStage{v + w * 4 * WAVE, l + w * 4 * WAVE, lane, slot},
                          LdsStage{v + LDS_STAGE1 + w * 4 * WAVE, l + LDS_STAGE1 + w * 4 * WAVE, lane, slot}, pr);
     } else {
-        siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf, pr);
+        siso<ALGO, (ALGO ? WIN_LM : 4), RAG>(in, out, N, ck, ring, cs, lane, sf);
     }
 }
 
@@ -1735,37 +1311,23 @@ struct DecodeArgs {
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
-    int row_pad;             // lanes of padding after each workspace row (0 unless TDEC_ROW_PAD)
     double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
     int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
     int ck_rows;             // checkpoint rows before the beta1 ring: ceil(N / ck_win_of(algo))
-    int *simd_prog = nullptr;   // TDEC_PRIO 4: [8192 SIMDs][16 wave slots] progress, zeroed per launch
-    // Item queue (TDEC_ITEMQ; null: each wave decodes whole tiles): work items are
-    // (tile, iteration).  A tile's first iteration is claimed from the chip-wide
-    // counter iq_ctl[0]; each later one is pushed to the claiming wave's XCD and
-    // taken by any wave of that XCD, so waves that run faster (alone on their SIMD,
-    // or idle at the end) take over iterations of the tiles of slower ones.  Le2
-    // then lives per TILE (le2t, [n_tiles][N][64]), handed from wave to wave inside
-    // one XCD (its L2 is shared; the taker invalidates its CU's L1 first).
-    // iq_ctl (zeroed per launch): [0] fresh-tile counter, then per XCD x at
-    // 32 * (x + 1): [0] tiles claimed, [1] items pushed, [2] items taken, [3] waves waiting;
-    // iq_ring [8][iq_cap]: entries tile * iters + iteration + 1 (0 = not yet written).
-    double2 *le2t = nullptr;
-    int *iq_ctl = nullptr;
-    int *iq_ring = nullptr;
-    int iq_cap = 0;
-    // The launch's tail (whole-tile mode): each wave, when it takes its last tile,
-    // raises *tail_flag to tail_seq (atomicMax; seq grows per launch), which
-    // k_tail_gate waits for (tdec_tail_gate: the next batch's demap is released
-    // into the slots the retiring waves free, not before the grid is placed).
+    int *simd_prog = nullptr;   // max-log issue priority: [8192 SIMDs][16 wave slots] progress, zeroed per launch
+    // The launch's tail: once the last tile has been handed out (the dynamic tile
+    // counter is exhausted, or, with static striding, the wave of the highest tile
+    // starts it) that wave raises *tail_flag to tail_seq (atomicMax; seq grows per
+    // launch), which k_tail_gate waits for (tdec_tail_gate: the next batch's demap
+    // is released into the slots the retiring waves free, not before the grid is
+    // placed).  Approximate by nature: with static striding other waves may still
+    // be starting their last tiles of the same round, and a launch captured in a
+    // graph keeps its tail_seq, so on replay the gate finds the flag already raised.
     unsigned *tail_flag = nullptr;
     unsigned tail_seq = 0;
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
-#ifndef TDEC_EPI_LDS
-#define TDEC_EPI_LDS 1
-#endif
 // Where a tile's planes come from.  PlanesIn: the caller's plane buffer
 // (tdec_decode_planes_dev); fill / publish are no-ops.  The fused demap
 // (DemapPro, below) fills a wave's next tile piece by piece between the SISOs of
@@ -1780,108 +1342,20 @@ struct PlanesIn {
 };
 
 // TDEC_WAVE_TIMING (measurement build): per persistent wave of the last decode
-// launch, {first, last} s_memrealtime (100 MHz, chip-wide) and the tiles it
-// took, printed by tdec_destroy: how much of the launch the waves spend idle
-// in the tail once the tile queue is empty.
+// launch, {first, last} s_memrealtime (100 MHz, chip-wide) and {first, last}
+// s_memtime (shader clock), the tiles it took and its HW_ID / XCC_ID, printed by
+// tdec_destroy (TDEC_WAVE_DUMP: per wave, tools/wave_dump.py): how much of the
+// launch the waves spend idle in the tail, and the clock each wave ran at
+// (shader ticks / real time).
 #ifndef TDEC_WAVE_TIMING
 #define TDEC_WAVE_TIMING 0
 #endif
 #if TDEC_WAVE_TIMING
 constexpr int WT_MAX = 16384;
-__device__ unsigned long long g_wave_t[WT_MAX][2];
+__device__ unsigned long long g_wave_t[WT_MAX][4];   // realtime start, end; memtime start, end
 __device__ int g_wave_tiles[WT_MAX];
 __device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of each wave
 #endif
-
-// Issue priority (TDEC_PRIO).  The two waves of a SIMD otherwise issue oldest
-// first: with one tile each (a batch of at most one round of tiles, e.g.
-// configs[1]) the older finishes its tile in ~7.7 ms and the younger runs the
-// last ~3 ms alone at the one-wave rate, 10.7 ms in all (profiles/r03p/).
-// Policy 1, s_setprio 3..0 over the four quarters of the tile's iterations,
-// hands the issue slots to whichever wave is behind by a quarter: configs[1]
-// 10.6 -> 10.1 ms per 102 400 codewords, 1 M codewords at 752 couples 244.3 ->
-// 238.5 ms (profiles/r03t/).  Policy 4 (default) compares against the other
-// wave of the SIMD every half SISO (per-SIMD progress slots, mate_prio above),
-// so the lag is half a SISO instead of a quarter tile: configs[1] 10.15 -> 9.8-9.9
-// ms, 1 M codewords 243.9 -> 237.3 ms against policy 1 (profiles/r03z/, both
-// orders).  Same bits under every policy; policies 2 / 3 (by pass) measured no
-// better than 1 (profiles/r03x/).
-__device__ __forceinline__ void progress_prio(int it, int iters) {
-    if constexpr (TDEC_PRIO == 1) set_prio(3 - (4 * it) / iters);
-}
-
-// ---- the (tile, iteration) item queue (DecodeArgs::le2t) -------------------------------
-__device__ __forceinline__ int iq_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ int iq_add(int *p, int v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Push item (this wave's XCD): reserve a ring slot, then write the entry (agent-scope
-// stores: the taker polls it past its L1).  Lane 0 only.
-// TDEC_IQ_YIELD: when a wave of the XCD is waiting for work, the pusher sleeps about
-// that many microseconds before it looks for its next item, so the waiting wave
-// (its SIMD otherwise idle) takes the pushed iteration and the pusher's SIMD sheds
-// a wave; without it the pusher nearly always takes its own item back.
-#ifndef TDEC_IQ_YIELD
-#define TDEC_IQ_YIELD 4
-#endif
-__device__ __forceinline__ void iq_push(const DecodeArgs &p, unsigned xcc, int lane, int item) {
-    bool yield = false;
-    if (lane == 0) {
-        int *c = p.iq_ctl + 32 * (xcc + 1);
-        const int slot = iq_add(c + 1, 1);
-        __hip_atomic_store(p.iq_ring + (long)xcc * p.iq_cap + slot, item + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        yield = TDEC_IQ_YIELD > 0 && iq_ld(c + 3) > 0;
-    }
-    if (__builtin_amdgcn_readfirstlane(yield ? 1 : 0))
-        for (int i = 0; i < 4 * TDEC_IQ_YIELD; ++i) __builtin_amdgcn_s_sleep(127);   // ~8k cycles: ~4 per us
-}
-// The wave's next item: a pushed iteration of this XCD's tiles first, else a fresh
-// tile (its iteration 0; the tile then belongs to this XCD), else -1 once every item
-// of this XCD has been taken and no fresh tile is left.  While items are in flight
-// on the XCD and none is ready the wave sleeps and polls; `spins` bounds that wait
-// (a wave that would wait ~seconds gives up rather than hang the device: the host
-// never relies on it, every item is taken by the wave that pushed it at the latest).
-__device__ int iq_next(const DecodeArgs &p, unsigned xcc, int lane, long &spins) {
-    int item = -1;
-    bool waiting = false;
-    if (lane == 0) {
-        int *c = p.iq_ctl + 32 * (xcc + 1);
-        int *ring = p.iq_ring + (long)xcc * p.iq_cap;
-        for (;;) {
-            const int taken = iq_ld(c + 2), pushed = iq_ld(c + 1);
-            if (taken < pushed) {
-                int expect = taken;
-                if (__hip_atomic_compare_exchange_strong(c + 2, &expect, taken + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) {
-                    int e;
-                    long w = 0;
-                    while ((e = iq_ld(ring + taken)) == 0 && ++w < (1L << 26)) __builtin_amdgcn_s_sleep(1);   // the pusher writes it next
-                    item = e - 1;
-                    break;
-                }
-                continue;
-            }
-            if (iq_ld(p.iq_ctl) < p.n_tiles) {
-                const int f = iq_add(p.iq_ctl, 1);
-                if (f < p.n_tiles) {
-                    iq_add(c, 1);
-                    item = f * p.iters;
-                    break;
-                }
-            }
-            // no fresh tile: done once every continuation of this XCD's tiles is taken
-            if (taken >= (p.iters - 1) * iq_ld(c)) break;
-            if (++spins > (1L << 24)) break;
-            if (!waiting) {
-                iq_add(c + 3, 1);   // this XCD has a wave waiting for work
-                waiting = true;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-        if (waiting) iq_add(c + 3, -1);
-    }
-    return __builtin_amdgcn_readfirstlane(item);
-}
 
 template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
@@ -1894,7 +1368,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     const int N = p.N;
     const long NW = (long)N * WAVE;
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
-    const unsigned rs = (unsigned)p.n_waves * WAVE + (unsigned)p.row_pad;
+    const unsigned rs = (unsigned)p.n_waves * WAVE;
     double2 *P1 = p.ws + (long)wave * WAVE * WS_G, *Le2 = P1 + (long)rows_of(N) * rs, *Le1 = Le2 + (long)rows_of(N) * rs;
     const int nw = p.ck_rows;
     float4 *ck = p.ck + (long)wave * WAVE * WS_G;
@@ -1902,13 +1376,13 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     double2 *sink = p.aux + WAVE + (long)wave * WAVE;
     int buf = 0;
 #if TDEC_WAVE_TIMING
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime(), wc0 = __builtin_amdgcn_s_memtime();
     int wtiles = 0;
 #endif
     pro.fill(wave, wave, N, 0, 0, 1);   // the first tile whole; later ones during the previous tile
     pro.publish();
     Prio pr;
-    if (TDEC_PRIO == 4 && p.simd_prog) {
+    if (p.simd_prog) {
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
         const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
         const unsigned key = ((xcc & 7u) << 10) | (((hw >> 13) & 7u) << 7) | (((hw >> 12) & 1u) << 6) |
@@ -1920,78 +1394,52 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     // taken from a queue (one atomic per tile from lane 0, issued at the tile's
     // start, consumed at its end), so waves whose codewords take longer (longer
     // merge passes) take fewer tiles and all waves finish close together.
-    // With the item queue (p.le2t) every trip of this loop is one (tile, iteration)
-    // item from iq_next instead.  One copy of the SISO call sites serves both forms
+    // (A queue of (tile, iteration) items instead of whole tiles, per-XCD rings with
+    // Le2 handed between waves, measured no faster: DESIGN.md, appendix.)
+    // One trip of this loop per (tile, iteration); the SISO call sites exist once
     // (the kernel's instruction footprint is shared by the CU's waves).
-    const bool iq = p.le2t != nullptr;
-    const unsigned xcc = iq ? (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
     int tile = wave, it = 0, nxt = 0;
     bool has_next = false;
-    long spins = 0;
     for (;;) {
-        if (iq) {
-            const int item = iq_next(p, xcc, lane, spins);
-            if (item < 0) break;
-            tile = item / p.iters;
-            it = item - tile * p.iters;
-            if (it > 0) {
-                // take over the tile's Le2 from the wave of this XCD that wrote it:
-                // this CU's L1 may hold older lines of those rows
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tile >= p.n_tiles) break;
+        if (it == 0) {
+            nxt = tile + p.n_waves;
+            if (p.tile_ctr) {
+                int q = 0;
+                if (lane == 0) q = atomicAdd(p.tile_ctr, 1);
+                nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
             }
-        } else {
-            if (tile >= p.n_tiles) break;
-            if (it == 0) {
-                nxt = tile + p.n_waves;
-                if (p.tile_ctr) {
-                    int q = 0;
-                    if (lane == 0) q = atomicAdd(p.tile_ctr, 1);
-                    nxt = p.n_waves + __builtin_amdgcn_readfirstlane(q);
-                }
-                has_next = nxt < p.n_tiles;
-                if (!has_next && p.tail_flag && lane == 0) atomicMax(p.tail_flag, p.tail_seq);
-            }
+            has_next = nxt < p.n_tiles;
+            if (p.tail_flag && lane == 0 && (p.tile_ctr ? !has_next : tile == p.n_tiles - 1))
+                atomicMax(p.tail_flag, p.tail_seq);
         }
         const float *base = pro.tile_planes(tile, wave, N, buf);
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
-        double2 *L2 = iq ? p.le2t + (long)tile * NW : Le2;   // this tile's Le2 rows
-        const unsigned rs2 = iq ? (unsigned)WAVE : rs;
         {
-            progress_prio(it, p.iters);
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            pr.hi = 2 * it < p.iters ? 3 : 1;
-            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? L2 : p.aux, inv, lane, it ? rs2 : 0u},
-                                TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs, lane, sf,
-                                lv, ll, pr);
+            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
+                                        TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs,
+                                        lane, sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
-            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{L2, lane, rs2}, N, ck, ring, rs, lane,
+            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
                                         sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
         if (it < p.iters - 1) {
-            if (iq) {
-                // hand the next iteration to this XCD's queue once every Le2 store of
-                // this wave has reached the XCD's L2
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                iq_push(p, xcc, lane, tile * p.iters + it + 1);
-            } else {
-                ++it;
-            }
+            ++it;
             continue;
         }
         unsigned long long tepi = TDEC_PASS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
-        // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm]
-        const long cw = (long)tile * WAVE + lane;
-#if TDEC_EPI_LDS
+        // hard decision (:526-537): L = (Lc + La) + Le1, La = Le2[inv_perm].
         // Bits of 32 couples per lane are packed into two LDS words, then the wave
         // writes the 64 rows chunk by chunk in row order (16-B int4 stores, each
         // wave store one contiguous 1 KiB run) instead of one 8-B store per lane
         // per couple 6 KB apart.
+        const long cw = (long)tile * WAVE + lane;
         uint32_t *hb = epi + (threadIdx.x >> 6) * epi_stride;
         const long nb = 2L * N;
         for (int kc = 0; kc < N; kc += 32) {
@@ -2008,7 +1456,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
                     const int k = min(kc + kg + u, N - 1);   // past the chunk: a valid row, unused
                     const float4 x = at(X, k * WAVE + lane);
                     xa[u] = make_float2(x.x, x.y);
-                    la[u] = at(L2, wsrow(inv[k], rs2) + lane);
+                    la[u] = at(Le2, wsrow(inv[k], rs) + lane);
                     le[u] = at(Le1, wsrow(k, rs) + lane);
                 }
 #pragma unroll
@@ -2046,38 +1494,22 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-#else
-        if (cw < p.B) {
-            int32_t *bo = p.bits + cw * 2 * N;
-            double *lo = p.lfinal ? p.lfinal + cw * 2 * N : nullptr;
-            for (int k = 0; k < N; ++k) {
-                const float4 x = X[(long)k * WAVE + lane];
-                const double2 la = L2[wsrow(inv[k], rs2) + lane];
-                const double2 le = Le1[wsrow(k, rs) + lane];
-                const double fa = ((double)x.x + la.x) + le.x;
-                const double fb = ((double)x.y + la.y) + le.y;
-                *reinterpret_cast<int2 *>(bo + 2 * k) = make_int2(fa < 0.0 ? 1 : 0, fb < 0.0 ? 1 : 0);
-                if (lo) *reinterpret_cast<double2 *>(lo + 2 * k) = make_double2(fa, fb);
-            }
-        }
-#endif
         pass_mark(tepi, 4);
-        if (!iq) {
-            if (has_next) pro.publish();
-            buf ^= 1;
-            tile = nxt;
-            it = 0;
-        }
+        if (has_next) pro.publish();
+        buf ^= 1;
+        tile = nxt;
+        it = 0;
 #if TDEC_WAVE_TIMING
         ++wtiles;
 #endif
     }
-    if (TDEC_PRIO == 4 && pr.tab && lane == 0)
-        __hip_atomic_store(pr.tab + pr.me, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pr.tab && lane == 0) __hip_atomic_store(pr.tab + pr.me, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if TDEC_WAVE_TIMING
     if (lane == 0 && wave < WT_MAX) {
         g_wave_t[wave][0] = wt0;
         g_wave_t[wave][1] = __builtin_amdgcn_s_memrealtime();
+        g_wave_t[wave][2] = wc0;
+        g_wave_t[wave][3] = __builtin_amdgcn_s_memtime();
         g_wave_tiles[wave] = wtiles;
         g_wave_hw[wave][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
         g_wave_hw[wave][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
@@ -2089,27 +1521,19 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 // values that do not fit go to scratch, outside the trellis loops.  log-MAP
 // spills more (its max* needs the registers), but a second wave per SIMD still
 // beats the one-wave VALU issue limit by a third.
-#ifndef TDEC_ML_WPE
-#define TDEC_ML_WPE 2
-#endif
+// (Three waves per SIMD for log-MAP -- 168 VGPRs, loops without spills -- measured
+// slower: 141.9 vs 122.3 ms per 262 144 codewords, profiles/r05/lm3_ab/.)
+constexpr int DEC_WPE = 2;
 template <bool RAG>
-__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_ML_WPE))) void k_turbo_decode(
+__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ float4 lv[LDS_LV];
     __shared__ double2 ll[LDS_STAGE];
-    if constexpr (TDEC_WIN_ML == 8) {
-        turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
-                                   EPI_STRIDE_ML);
-    } else {
-        __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
-        turbo_decode_tiles<0, RAG>(p, perm, inv, used, lv, ll, epi, PlanesIn{p.planes});
-    }
+    turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
+                                     EPI_STRIDE_ML);
 }
-#ifndef TDEC_LM_WPE
-#define TDEC_LM_WPE 2   // 2 waves/SIMD with some scratch: +33 % over the compiler's 1-wave budget (measured)
-#endif
 template <bool RAG>
-__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_turbo_decode_logmap(
+__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
     turbo_decode_tiles<1, RAG>(p, perm, inv, used, nullptr, nullptr, epi, PlanesIn{p.planes});
@@ -2150,7 +1574,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(2))) void
     siso_rows<0, RAG, F64>(p);
 }
 template <bool RAG, bool F64 = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(TDEC_LM_WPE))) void k_siso_batch_logmap(
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_siso_batch_logmap(
     SisoArgs p) {
     siso_rows<1, RAG, F64>(p);
 }
@@ -2201,7 +1625,7 @@ struct DemapCfg {
     double nv;                 // max(noise_var, 0.005) already applied (:202)
     int sep;                   // 1: separable square QAM grid (per-axis levels follow the points);
                                // 2: and each axis a Gray-labelled uniform PAM (position-ordered levels follow)
-    int nv_fast;               // nv in [2^-8, 2^16]: the unscaled f32 / f64 division (TDEC_DM_FAST64)
+    int nv_fast;               // nv in [2^-8, 2^16]: the unscaled f32 / f64 division (dm_fast)
 };
 __host__ __device__ inline int dm_nv_fast(double nv) { return nv >= 0x1p-8 && nv <= 0x1p16; }
 // LDS table: 2*M point coordinates (+ 2 * 2^(bps/2) axis levels in label order; for a
@@ -2209,7 +1633,7 @@ __host__ __device__ inline int dm_nv_fast(double nv) { return nv >= 0x1p-8 && nv
 // parameters and the 2 * K * 2^K neighbour positions of sym_llrs_gray)
 constexpr int DM_TAB = 768;
 
-// TDEC_DM_FAST64 (f64 tables): the compiler's own f64 division and square root
+// The unscaled sequences (dm_fast): the compiler's own f64 division and square root
 // sequences without their range scaling, where the scaling is provably the
 // identity -- the same instructions on the same values, so the same bits:
 //   a / b: v_div_scale (identity) -> r = v_rcp_f64(b), two Newton steps
@@ -2224,16 +1648,9 @@ constexpr int DM_TAB = 768;
 // Outside those ranges the compiler's sequences run (a branch no lane takes on
 // ordinary symbols).  tdec_selftest 4 compares both against the compiler's
 // sequences on random operands over the ranges the demapper meets.
-#ifndef TDEC_DM_FAST64
-#define TDEC_DM_FAST64 1
-#endif
 // BPSK .. 16QAM (measured faster, profiles/r05/demap_ab/); the 64 / 256QAM kernels
 // keep the compiler's sequences (their registers grow past an occupancy step)
-__host__ __device__ constexpr bool dm_fast(int bps) { return TDEC_DM_FAST64 && bps <= 4; }
-// TDEC_DM_PAIRS: 16QAM's per-axis search as pair minima (sym_llrs_sep)
-#ifndef TDEC_DM_PAIRS
-#define TDEC_DM_PAIRS 1
-#endif
+__host__ __device__ constexpr bool dm_fast(int bps) { return bps <= 4; }
 __device__ __forceinline__ double rcp_nr64(double b) {   // v_div_scale-free reciprocal of the division sequence
     double r = __builtin_amdgcn_rcp(b);
     r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
@@ -2294,7 +1711,7 @@ __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
     if (sizeof(T) == 4 && c.div_f32) {
         // the f32 quotient clipped and negated in f32: the same values as in f64
         // (f32 -> f64 is exact and so are the +-30 clip and the negation)
-        // TDEC_DM_FAST64: nv in [2^-8, 2^16], |diff| in [2^-90, 2^60]: nothing scaled
+        // dm_fast: nv in [2^-8, 2^16], |diff| in [2^-90, 2^60]: nothing scaled
         const float fd = (float)diff, fn = (float)c.nv, af = fabsf(fd);
         float q = FAST && c.nv_fast && af >= 0x1p-90f && af <= 0x1p60f ? div_nr32(fd, fn, rcp_nr32(fn))
                                                                                   : fd / fn;
@@ -2303,7 +1720,7 @@ __device__ __forceinline__ double llr_from_diff(T diff, const DemapCfg &c) {
     }
     double v;
     const double dd = (double)diff, ad = fabs(dd);
-    // TDEC_DM_FAST64: nv in [2^-8, 2^16] (host flag) and |diff| in [2^-900, 2^600]:
+    // dm_fast: nv in [2^-8, 2^16] (host flag) and |diff| in [2^-900, 2^600]:
     // no operand or quotient the division sequence would scale (zero, whose sign
     // v_div_fixup sets, NaN and inf take the compiler's division)
     if (FAST && c.nv_fast && ad >= 0x1p-900 && ad <= 0x1p600) v = div_nr64(dd, c.nv, rcp_nr64(c.nv));
@@ -2371,7 +1788,7 @@ template <typename T, bool FAST = false, bool PRE = false> __device__ __forceinl
     return sqrt_1_2<T>(fma(ratio, ratio, (T)1)) * larger;
 }
 
-// TDEC_DM_PAIRS (16QAM, nv_fast): the per-axis search below for K = 2 in closed
+// 16QAM (nv_fast): the per-axis search below for K = 2 in closed
 // form, carrying the differences instead of level indices.  Every bit-half holds
 // two levels ({0, 1} / {2, 3} for the label's high bit, {0, 2} / {1, 3} for its
 // low bit), so its nearest / second nearest / first argmin are a min / max /
@@ -2460,7 +1877,7 @@ __device__ __forceinline__ bool sym_llrs_sep(T sr, T si, const T *cons, const De
     const T *lev_i = cons + 2 * (1 << BPS), *lev_q = lev_i + L;
     const T inf = (T)INFINITY;
     const T eps = sizeof(T) == 4 ? (T)3.8e-6 : (T)7.2e-15, tau = sizeof(T) == 4 ? (T)1e-30 : (T)1e-290;
-    if constexpr (K == 2 && TDEC_DM_PAIRS && dm_fast(BPS)) {
+    if constexpr (K == 2 && dm_fast(BPS)) {
         if (c.nv_fast) return sym_llrs_pairs16<T, F32OUT>(sr, si, cons, c, out);
     }
     T all1[2], all2[2], b1[2][K][2], b2[2][K][2];   // nearest / second nearest: axis, bit-halves
@@ -2569,7 +1986,7 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
         out[b] = llr_of<T, dm_fast(BPS)>(n0[b] ? (T)NAN : m0[b], n1[b] ? (T)NAN : m1[b], c);   // np.min propagates NaN
 }
 
-// TDEC_DM_SCANPRE (BPSK / QPSK / 8PSK, finite symbols): the scan with the
+// sym_llrs_scan_pre (BPSK / QPSK / 8PSK, finite symbols): the scan with the
 // unscaled division / square root under one range test per symbol instead of one
 // per point (sym_llrs_pairs16): every point's larger |difference| within [2^-80,
 // 2^29] (f32) / [2^-800, 2^290] (f64) and nv_fast, for every lane of the wave, or
@@ -2578,15 +1995,10 @@ __device__ __forceinline__ void sym_llrs_scan(T sr, T si, const T *cons, const D
 // of zero or below the quotient's range takes the compiler's division (its sign of
 // zero), per lane.  Measured (profiles/r05/demap_scan/, same planes): 8PSK
 // 12.66 -> 11.61 ms, QPSK 5.88 -> 5.70 ms per 1 M codewords.
-#ifndef TDEC_DM_SCANPRE
-#define TDEC_DM_SCANPRE 1
-#endif
-// TDEC_DM_F32OUT: the plane kernels take the LLRs' f32 form (llr_from_diff F32OUT):
+// The plane kernels take the LLRs' f32 form (llr_from_diff F32OUT = DM_F32OUT):
 // same planes, 16QAM 12.62 -> 12.29 ms, 256QAM 12.82 -> 12.30, 8PSK 11.27 -> 11.11 per
 // 1 M codewords (profiles/r05/demap_f32out/)
-#ifndef TDEC_DM_F32OUT
-#define TDEC_DM_F32OUT 1
-#endif
+constexpr bool DM_F32OUT = true;
 template <typename T, int BPS, bool F32OUT = false, int M = (1 << BPS)>
 __device__ __forceinline__ bool sym_llrs_scan_pre(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     constexpr bool F32 = sizeof(T) == 4;
@@ -2633,7 +2045,7 @@ template <typename T, int BPS, bool F32OUT = false, int M = (1 << BPS)>
 __device__ __forceinline__ void sym_llrs(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
     if constexpr (M <= 8) {
         if (__all(isfinite(sr) && isfinite(si))) {
-            if constexpr (TDEC_DM_SCANPRE && dm_fast(BPS)) {
+            if constexpr (dm_fast(BPS)) {
                 if (sym_llrs_scan_pre<T, BPS, F32OUT>(sr, si, cons, c, out)) return;
             }
             sym_llrs_scan<T, BPS, true>(sr, si, cons, c, out);
@@ -2731,9 +2143,6 @@ __device__ __forceinline__ bool sym_llrs_sep_seq(T sr, T si, const T *cons, cons
 // each bit-half is unique and is the candidate, so the LLRs are the full scan's bit
 // for bit; anything else (non-finite input, near ties, a wrong position estimate)
 // returns false and the caller scans.
-#ifndef TDEC_DM_GRAYPRE
-#define TDEC_DM_GRAYPRE 1
-#endif
 __device__ __forceinline__ int gray_inv(int q, int K) {
     int a = q;
     for (int sh = 1; sh < K; ++sh) a ^= q >> sh;
@@ -2776,56 +2185,37 @@ __device__ __forceinline__ bool sym_llrs_gray(T sr, T si, const T *cons, const D
     }
     const T tol = eps * (2 * dmax) + tau;
     if (!(dmax < inf && gapmin > tol)) return false;
-    if constexpr (TDEC_DM_GRAYPRE) {
-        // (a noise variance outside [2^-8, 2^16] declines every symbol to the
-        // callers' other searches: the compiler's sequences below would hold their
-        // registers in this kernel too, a step of occupancy)
-        if (!c.nv_fast) return false;
-        {
-            // TDEC_DM_GRAYPRE: the differences the search formed, and one range test
-            // per symbol for the unscaled division / square root (sym_llrs_pairs16):
-            // every candidate's larger |difference| lies between the axes' nearest
-            // differences and sqrt(dmax); outside, or an LLR numerator below the
-            // quotient's range, the symbol declines to the full chain
-            constexpr bool F32 = sizeof(T) == 4;
-            const T l0 = fmax(fabs(e0s[0]), fabs(e0s[1]));
-            if (!(l0 >= (F32 ? (T)0x1p-80f : (T)0x1p-800) && dmax <= (F32 ? (T)0x1p58f : (T)0x1p580))) return false;
-            const T an = cabs_fin<T, true, true>(e0s[0], e0s[1]);
-            const T dq = an * an;
-            const T lo = F32 ? (c.div_f32 ? (T)0x1p-90f : (T)0x1p-149f) : (T)0x1p-900;
-            T diff[BPS], dlo = inf;
-#pragma unroll
-            for (int ax = 0; ax < 2; ++ax) {
-                const int lab = gray_inv(p[ax], K);
-#pragma unroll
-                for (int b = 0; b < K; ++b) {
-                    const int vn = (lab >> (K - 1 - b)) & 1;
-                    const T a = ax ? cabs_fin<T, true, true>(e0s[0], cds[1][b]) : cabs_fin<T, true, true>(cds[0][b], e0s[1]);
-                    const T ao = a * a;
-                    diff[ax * K + b] = vn ? ao - dq : dq - ao;   // m[0] - m[1], m[vn] = dn
-                    dlo = fmin(dlo, fabs(diff[ax * K + b]));
-                }
-            }
-            if (!(dlo >= lo)) return false;
-#pragma unroll
-            for (int k = 0; k < BPS; ++k) out[k] = llr_from_diff<T, true, true, F32OUT>(diff[k], c);
-            return true;
-        }
-    }
-    const T an = cabs_fin<T, dm_fast(BPS)>(sr - pos_i[p[0]], si - pos_q[p[1]]);
-    const T dn = an * an;
+    // (a noise variance outside [2^-8, 2^16] declines every symbol to the
+    // callers' other searches: the compiler's sequences would hold their
+    // registers in this kernel too, a step of occupancy)
+    if (!c.nv_fast) return false;
+    // the differences the search formed, and one range test per symbol for the
+    // unscaled division / square root (sym_llrs_pairs16): every candidate's larger
+    // |difference| lies between the axes' nearest differences and sqrt(dmax);
+    // outside, or an LLR numerator below the quotient's range, the symbol declines
+    // to the full chain
+    constexpr bool F32 = sizeof(T) == 4;
+    const T l0 = fmax(fabs(e0s[0]), fabs(e0s[1]));
+    if (!(l0 >= (F32 ? (T)0x1p-80f : (T)0x1p-800) && dmax <= (F32 ? (T)0x1p58f : (T)0x1p580))) return false;
+    const T an = cabs_fin<T, true, true>(e0s[0], e0s[1]);
+    const T dq = an * an;
+    const T lo = F32 ? (c.div_f32 ? (T)0x1p-90f : (T)0x1p-149f) : (T)0x1p-900;
+    T diff[BPS], dlo = inf;
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax) {
         const int lab = gray_inv(p[ax], K);
 #pragma unroll
         for (int b = 0; b < K; ++b) {
             const int vn = (lab >> (K - 1 - b)) & 1;
-            const T a = ax ? cabs_fin<T, dm_fast(BPS)>(sr - pos_i[p[0]], si - pos_q[cb[1][b]])
-                           : cabs_fin<T, dm_fast(BPS)>(sr - pos_i[cb[0][b]], si - pos_q[p[1]]);
+            const T a = ax ? cabs_fin<T, true, true>(e0s[0], cds[1][b]) : cabs_fin<T, true, true>(cds[0][b], e0s[1]);
             const T ao = a * a;
-            out[ax * K + b] = llr_from_diff<T, dm_fast(BPS)>(vn ? ao - dn : dn - ao, c);   // m[0] - m[1], m[vn] = dn
+            diff[ax * K + b] = vn ? ao - dq : dq - ao;   // m[0] - m[1], m[vn] = dn
+            dlo = fmin(dlo, fabs(diff[ax * K + b]));
         }
     }
+    if (!(dlo >= lo)) return false;
+#pragma unroll
+    for (int k = 0; k < BPS; ++k) out[k] = llr_from_diff<T, true, true, F32OUT>(diff[k], c);
     return true;
 }
 
@@ -2848,12 +2238,9 @@ __device__ __forceinline__ void dm_count(int, int) {}
 #endif
 template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ void demap_sym(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
-#ifndef TDEC_DM_GRAY
-#define TDEC_DM_GRAY 1
-#endif
     // 64 / 256QAM (measured, 1 M codewords, same planes: 20.2 -> 17.6 ms, 70.3 -> 56.2 ms);
     // 16QAM's 4-level scan is cheaper than the table lookups (14.9 vs 16.0 ms)
-    if constexpr (TDEC_DM_GRAY && BPS >= 6 && BPS % 2 == 0) {
+    if constexpr (BPS >= 6 && BPS % 2 == 0) {
         if (c.sep == 2 && sym_llrs_gray<T, BPS, F32OUT>(sr, si, cons, c, out)) return dm_count(1, c.sep);
     }
     if constexpr (BPS >= 8 && BPS % 2 == 0) {
@@ -2926,7 +2313,7 @@ __global__ __launch_bounds__(BLOCK) void k_selftest(int which, long long n, unsi
             ok = ok && hw_exp2(qn) != hw_exp2(qn) && hw_log2(qn) != hw_log2(qn) && __float_as_uint(hw_log2(1.0f)) == 0u;
         }
     } else if (which == 4) {
-        // TDEC_DM_FAST64's sequences against the compiler's on the demapper's ranges:
+        // the unscaled sequences (dm_fast) against the compiler's on the demapper's ranges:
         // |z| of (re, im) with exponents in [-64, 16) (a quarter of the items with
         // |im| within a factor 2 of |re|); a / b with |a| in [2^-900, 2^600), b in
         // [2^-8, 2^100); sqrt on [1, 2)
@@ -2973,17 +2360,16 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 }
 
 // Fused demap -> f32 -> de-puncture planes (the bench path).
-// One item = one 64-codeword tile x DM_KC trellis steps (a block loops over
-// items, TDEC_DM_BPC).  Phase 1: the block's threads demap every symbol covering the LLR range of those steps
-// (couples consume LLRs in order, so the range is contiguous) into an LDS
-// tile [64 codewords][range], decoder sign, rounded to f32 as decode() does
-// (:466).  Phase 2: each thread assembles whole plane entries
-// X[k] = {A, B, W1, Y1} (float4), Z[k] = {W2, Y2} (float2) and stores them
-// coalesced; punctured or missing LLRs are 0.0
+// One item = one 64-codeword tile x DM_KC trellis steps (one block per item).
+// Phase 1: the block's threads demap every symbol covering the LLR range of those
+// steps (couples consume LLRs in order, so the range is contiguous) into an LDS
+// tile, decoder sign, rounded to f32 as decode() does (:466).  Phase 2: each
+// thread assembles whole plane entries X[k] = {A, B, W1, Y1} (float4), Z[k] =
+// {W2, Y2} (float2) and stores them coalesced; punctured or missing LLRs are 0.0
 // (:469-474; the harness pads to n_coded, test_sdr_with_coding.py:474-478).
 // src[c*N + k] = LLR index of plane component c (X.xyzw, -, -, Z.xy) or -1;
 // off[k] = first LLR index of couple k (off[N] = n_llr).
-// TDEC_DM_SPLIT (round 4, square 16 / 64 / 256QAM): k_demap_planes runs only the
+// Split tables (round 4, square 16 / 64 / 256QAM): k_demap_planes runs only the
 // fast exact search (the Gray positions for 64 / 256QAM, the per-axis search for
 // 16QAM) and appends the symbols it declines (near ties, non-finite input, a
 // non-separable table: 0.02-0.08 % of them at 2 dB) to a list in HBM; k_demap_fix
@@ -2991,73 +2377,28 @@ __global__ __launch_bounds__(BLOCK) void k_trans_table(int which, unsigned lo, l
 // entries.  The fallbacks' registers (256QAM: 148 VGPRs and 311 SGPR spills with
 // them inline, three waves per SIMD) are then not the main kernel's.  A tile whose
 // declines overflow the list is flagged and k_demap_fix redoes all of its symbols.
-// Same planes: every path returns the scan's LLRs.  (Round 4's first form, the
-// fallback in a second loop of the same kernel, TDEC_DM_LEAN, kept the registers
-// and was 2.3x slower on 256QAM, profiles/r04e/ab_demap_*.)
-#ifndef TDEC_DM_SPLIT
-#define TDEC_DM_SPLIT 1
-#endif
-// TDEC_DM_PERSIST (build variant): k_demap_planes' grid is the device's resident
-// blocks, each looping over (tile, chunk) items with its table loaded once,
-// instead of one block per item.  Measured slower on every table
-// (profiles/r04f/ab_demap_*: 256QAM 59.0 vs 57.0 ms, 16QAM 19.3 vs 16.9 ms per
-// 1 M codewords): the table upload is not what the kernel waits on.
-#ifndef TDEC_DM_PERSIST
-#define TDEC_DM_PERSIST 0
-#endif
-#ifndef TDEC_DM_PF
-#define TDEC_DM_PF 1
-#endif
-// TDEC_DM_KC: couples per block (its LDS tile [64][6 * KC + 2 * BPS + 1] f32 bounds
-// the blocks per CU: 16 -> 27-29 KB, five)
-#ifndef TDEC_DM_KC
-#define TDEC_DM_KC 16
-#endif
-// TDEC_DM_KC_QPSK: QPSK's (its kernel is LDS-bound at five blocks per CU, and its
-// work per block small: 12 couples measured faster, 5.47 vs 5.82 ms per 1 M N = 212
-// codewords; 16QAM slower with 12 or 8, 13.45 / 13.41 vs 12.75 ms,
-// profiles/r05/demap_kc/)
-#ifndef TDEC_DM_KC_QPSK
-#define TDEC_DM_KC_QPSK 12
-#endif
-// TDEC_DM_EXP (timing builds only, WRONG PLANES): 1 = phase 1 without the demap
-// arithmetic, to split the kernel's time into its search / LLR work and the rest
-#ifndef TDEC_DM_EXP
-#define TDEC_DM_EXP 0
-#endif
-// TDEC_DM_PLANAR: the LDS tile by label bit (column b * ns + symbol), so the 64
-// lanes of a phase-1 store hit 64 banks: 1.5-4 % faster on every table, both A/B
-// orders (16QAM 12.08 vs 12.39 ms, QPSK 5.19 vs 5.37, profiles/r05/demap_planar/)
-#ifndef TDEC_DM_PLANAR
-#define TDEC_DM_PLANAR 1
-#endif
-// TDEC_DM_WAVE: each wave of a block owns 16 of the tile's 64 codewords, both
-// phases -- its LDS rows are its own, so the phases meet at no block barrier and
-// the waves of a CU drift apart (one wave's plane stores drain behind another's
-// search); phase 2 stores 4 x 256 B per instruction.  Measured slower on every
-// table (16QAM 13.95 vs 12.63 ms, QPSK 5.9-6.1 vs 5.37, profiles/r05/demap_wave/)
-#ifndef TDEC_DM_WAVE
-#define TDEC_DM_WAVE 0
-#endif
-// TDEC_DM_NOVMW (with TDEC_DM_PERSIST): the end-of-item barrier does not wait for
-// the plane stores -- measured slower (16QAM 15.1 vs 13.4 ms, profiles/r05/demap_planar/)
-#ifndef TDEC_DM_NOVMW
-#define TDEC_DM_NOVMW 0
-#endif
-constexpr int DM_KC = TDEC_DM_KC;          // couples per block
+// Same planes: every path returns the scan's LLRs.  (The fallback in a second loop
+// of the same kernel kept the registers and was 2.3x slower on 256QAM,
+// profiles/r04e/ab_demap_*; a persistent grid, one wave per 16 codewords, and the
+// other forms in the DESIGN.md appendix measured slower.)
+// KC: couples per block (its LDS tile [64][6 * KC + 2 * BPS + 1] f32 bounds the
+// blocks per CU: 16 -> 27-29 KB, five).  QPSK's kernel is LDS-bound at five blocks
+// per CU and its work per block small: 12 couples measured faster (5.47 vs 5.82 ms
+// per 1 M N = 212 codewords); 16QAM slower with 12 or 8 (13.45 / 13.41 vs 12.75 ms,
+// profiles/r05/demap_kc/).
+constexpr int DM_KC = 16;                  // couples per block
 constexpr int DM_MAXL = DM_KC * 6;         // max LLRs per chunk (6 per couple at rate 1/3)
-constexpr int DM_LD = DM_MAXL + 1;         // odd row stride: conflict-free column reads
-__host__ __device__ constexpr int dm_kc(int bps) { return bps == 2 ? TDEC_DM_KC_QPSK : TDEC_DM_KC; }
-__host__ __device__ constexpr bool dm_split(int bps) { return TDEC_DM_SPLIT && bps >= 4 && bps % 2 == 0; }
+__host__ __device__ constexpr int dm_kc(int bps) { return bps == 2 ? 12 : DM_KC; }
+__host__ __device__ constexpr bool dm_split(int bps) { return bps >= 4 && bps % 2 == 0; }
 
-// The decline list of k_demap_planes (TDEC_DM_SPLIT): entries {codeword, symbol},
+// The decline list of k_demap_planes (split tables): entries {codeword, symbol},
 // the entry count, and per-tile overflow flags.
 constexpr unsigned DM_DECL_CAP = 1u << 21;   // entries (16 MiB): 4x the declines of 1 M 256QAM codewords at 2 dB
 // A table takes the split path when its fast search can accept its symbols: the
 // Gray search (64 / 256QAM) needs sep == 2, 16QAM's per-axis search sep >= 1;
 // any other table would decline every symbol.
 __host__ __device__ constexpr bool dm_split_table(int bps, int sep) {
-    return dm_split(bps) && (bps >= 6 && TDEC_DM_GRAY ? sep == 2 : sep >= 1);
+    return dm_split(bps) && (bps >= 6 ? sep == 2 : sep >= 1);
 }
 struct DemapDecl {
     int2 *list;
@@ -3069,38 +2410,23 @@ struct DemapDecl {
 // the fast exact search of a split table; false: declined
 template <typename T, int BPS, bool F32OUT = false>
 __device__ __forceinline__ bool demap_fast(T sr, T si, const T *cons, const DemapCfg &c, double (&out)[BPS]) {
-    if constexpr (TDEC_DM_GRAY && BPS >= 6) return c.sep == 2 && sym_llrs_gray<T, BPS, F32OUT>(sr, si, cons, c, out);
+    if constexpr (BPS >= 6) return c.sep == 2 && sym_llrs_gray<T, BPS, F32OUT>(sr, si, cons, c, out);
     else return c.sep && sym_llrs_sep<T, BPS, F32OUT>(sr, si, cons, c, out);
 }
 
-// TDEC_DM_WPE: the plane kernels' minimum waves per SIMD (amdgpu_waves_per_eu: the
-// register budget 512 / WPE; 0 = the compiler's choice).  It binds only the f64
-// instances (complex128 tables: 133 / 141 / 169 VGPRs for 16 / 64 / 256QAM); the
-// complex64 tables the bench times hold 85 / 77 / 89 and are unchanged by it, so
-// the A/B in profiles/r05/demap_wpe/ (same times) measured nothing about them
-#ifndef TDEC_DM_WPE
-#define TDEC_DM_WPE 0
-#endif
-#if TDEC_DM_WPE > 0
-#define TDEC_DM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TDEC_DM_WPE)))
-#else
-#define TDEC_DM_WPE_ATTR
-#endif
 template <typename T, int BPS, bool SPLIT = false>
-__global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
+__global__ __launch_bounds__(BLOCK) void k_demap_planes(int B, int N, int S, const float *syms, const T *cons_g,
                                                        DemapCfg c, const int *__restrict__ src,
                                                        const int *__restrict__ off, long n_avail, float *planes,
                                                        long n_items, DemapDecl dd) {
     __shared__ T cons[DM_TAB];
-    // couples per item, LDS row stride (odd); TDEC_DM_PLANAR: the tile by label bit
-    // (column b * ns + symbol: the 64 lanes of a phase-1 store hit 64 banks) with room
-    // for the item's straddling symbols
-    constexpr int KC = dm_kc(BPS), LD = TDEC_DM_PLANAR ? 6 * KC + 2 * BPS + 1 : 6 * KC + 1;
+    // couples per item, LDS row stride (odd); the tile by label bit (column b * ns +
+    // symbol: the 64 lanes of a phase-1 store hit 64 banks, 1.5-4 % faster on every
+    // table, profiles/r05/demap_planar/) with room for the item's straddling symbols
+    constexpr int KC = dm_kc(BPS), LD = 6 * KC + 2 * BPS + 1;
     __shared__ float L[WAVE * LD];
     static_assert(!SPLIT || dm_split(BPS), "split only for square 16 / 64 / 256QAM");
-    constexpr bool WV = TDEC_DM_WAVE != 0;
-    constexpr int CPW = WAVE / (BLOCK / WAVE);   // TDEC_DM_WAVE: codewords per wave
-    const int wv = (int)threadIdx.x / WAVE, me = (int)threadIdx.x & (WAVE - 1);
+    const int me = (int)threadIdx.x & (WAVE - 1);
     load_table<T, BPS>(cons, cons_g, c);
     const int chunks = (N + KC - 1) / KC;
     __syncthreads();
@@ -3112,25 +2438,23 @@ __global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, 
         const long s0 = j0 / BPS, s1 = (j1 + BPS - 1) / BPS;        // symbols covering [j0, j1)
         const int ns = (int)(s1 - s0);
         // item t = (lane, si), consecutive threads: consecutive symbols; the
-        // quotient and remainder of t by ns advance by those of STEP each step
-        // (TDEC_DM_WAVE: t over the wave's own codewords, lanes LN0 + ...)
-        constexpr int STEP = WV ? WAVE : BLOCK, NL = WV ? CPW : WAVE;
-        const int T0 = WV ? me : (int)threadIdx.x, LN0 = WV ? wv * CPW : 0;
-        const int dq = STEP / ns, dr = STEP - dq * ns;
+        // quotient and remainder of t by ns advance by those of BLOCK each step
+        const int T0 = (int)threadIdx.x;
+        const int dq = BLOCK / ns, dr = BLOCK - dq * ns;
         int lane = T0 / ns, si = T0 - lane * ns;
-        const int nt = NL * ns;
+        const int nt = WAVE * ns;
         // the symbol of item t (lane ln, symbol sx), zero past the batch / the item's end
         auto sym_at = [&](int t, int ln, int sx) -> float2 {
             const long cw = tile * WAVE + ln, s = s0 + sx;
             return t < nt && cw < B && s < S ? *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s))
                                              : make_float2(0.0f, 0.0f);
         };
-        // TDEC_DM_PF: the next item's symbol is loaded before this one is demapped
-        // (8PSK / 16QAM: measured faster; QPSK and 64 / 256QAM slower)
-        constexpr bool PF = TDEC_DM_PF && (BPS == 3 || BPS == 4);
-        float2 zn = PF ? sym_at(T0, LN0 + lane, si) : make_float2(0.0f, 0.0f);
-        for (int t = T0; t < nt; t += STEP) {
-            const int ln = LN0 + lane, sx = si;
+        // the next item's symbol is loaded before this one is demapped (8PSK / 16QAM:
+        // measured faster; QPSK and 64 / 256QAM slower)
+        constexpr bool PF = BPS == 3 || BPS == 4;
+        float2 zn = PF ? sym_at(T0, lane, si) : make_float2(0.0f, 0.0f);
+        for (int t = T0; t < nt; t += BLOCK) {
+            const int ln = lane, sx = si;
             lane += dq;
             si += dr;
             if (si >= ns) {
@@ -3138,17 +2462,14 @@ __global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, 
                 ++lane;
             }
             const float2 zc = PF ? zn : sym_at(t, ln, sx);
-            if (PF) zn = sym_at(t + STEP, LN0 + lane, si);
+            if (PF) zn = sym_at(t + BLOCK, lane, si);
             const long cw = tile * WAVE + ln;
             const long s = s0 + sx;
             const bool live = cw < B && s < S;
             double v[BPS];
             if constexpr (SPLIT) {
                 bool dec = false;
-                if constexpr (TDEC_DM_EXP & 1) {   // timing only: no demap (the loaded symbol, written as LLRs)
-#pragma unroll
-                    for (int b = 0; b < BPS; ++b) v[b] = (double)(b & 1 ? zc.y : zc.x);
-                } else if (live) dec = !demap_fast<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
+                if (live) dec = !demap_fast<T, BPS, DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
                 // declined symbols go to the list for k_demap_fix (which rewrites their
                 // plane entries): one atomic per wave, entries by lane rank
                 const unsigned long long m = __ballot(dec);
@@ -3167,48 +2488,12 @@ __global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, 
                 if (!live || dec) continue;
             } else {
                 if (!live) continue;
-                demap_sym<T, BPS, TDEC_DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
+                demap_sym<T, BPS, DM_F32OUT>((T)zc.x, (T)zc.y, cons, c, v);
             }
 #pragma unroll
-            for (int b = 0; b < BPS; ++b) {
-                const long j = s * BPS + b;
-                if constexpr (TDEC_DM_PLANAR) L[ln * LD + b * ns + sx] = (float)v[b];
-                else if (j >= j0 && j < j1) L[ln * LD + (int)(j - j0)] = (float)v[b];
-            }
+            for (int b = 0; b < BPS; ++b) L[ln * LD + b * ns + sx] = (float)v[b];
         }
         float *base = planes + tile * tile_floats(N);
-        if constexpr (WV) {
-            // the wave reads back only rows its own lanes wrote: LDS operations of one
-            // wave complete in order, so a compiler barrier is all the ordering needed
-            asm volatile("" ::: "memory");
-            const int nk = k1 - k0;
-            for (int t = me; t < CPW * nk; t += WAVE) {   // float4 entries: 16 lanes x 4 steps
-                const int k = k0 + t / CPW, lane = LN0 + (t & (CPW - 1));
-                const long cw = tile * WAVE + lane;
-                float v[4];
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const int j = src[(long)cc * N + k];
-                    const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
-                    v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
-                }
-                reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
-            }
-            for (int t = me; t < CPW * nk; t += WAVE) {   // float2 entries
-                const int k = k0 + t / CPW, lane = LN0 + (t & (CPW - 1));
-                const long cw = tile * WAVE + lane;
-                float v[2];
-#pragma unroll
-                for (int cc = 0; cc < 2; ++cc) {
-                    const int j = src[(long)(6 + cc) * N + k];
-                    const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
-                    v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
-                }
-                reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
-            }
-            asm volatile("" ::: "memory");
-            continue;
-        }
         __syncthreads();
         for (int t = threadIdx.x; t < WAVE * (k1 - k0) * 2; t += BLOCK) {
             const int lane = t & (WAVE - 1);
@@ -3221,20 +2506,17 @@ __global__ __launch_bounds__(BLOCK) TDEC_DM_WPE_ATTR void k_demap_planes(int B, 
             for (int cc = 0; cc < 4; ++cc) {
                 if (cc >= nc) break;
                 const int j = src[(long)(half ? 6 + cc : cc) * N + k];
-                const int col = TDEC_DM_PLANAR ? (j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0) : (int)(j - j0);
+                const int col = j >= 0 ? (j % BPS) * ns + (int)(j / BPS - s0) : 0;
                 v[cc] = (j >= 0 && j < n_avail && cw < B) ? L[lane * LD + col] : 0.0f;
             }
             if (half == 0) reinterpret_cast<float4 *>(base)[(long)k * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
             else reinterpret_cast<float2 *>(base + (long)N * WAVE * 4)[(long)k * WAVE + lane] = make_float2(v[0], v[1]);
         }
-        // L is rewritten by the next item: its reads done everywhere (TDEC_DM_NOVMW: the
-        // plane stores keep draining behind the next item's phase 1)
-        if constexpr (TDEC_DM_NOVMW) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else __syncthreads();
+        __syncthreads();   // L is rewritten by the next item: its reads done everywhere
     }
 }
 
-// The declined symbols of k_demap_planes (TDEC_DM_SPLIT): demap_sym's whole chain,
+// The declined symbols of k_demap_planes (split tables): demap_sym's whole chain,
 // each LLR into its plane entry (dst[j] = c * N + k for the component c of couple
 // k that LLR j feeds, -1: none), then every symbol of an overflowed tile.
 template <typename T, int BPS>
@@ -3242,7 +2524,7 @@ __device__ __forceinline__ void dm_fix_symbol(long cw, long s, int N, int S, con
                                               const DemapCfg &c, const int *dst, long n_avail, float *planes) {
     const float2 z = *reinterpret_cast<const float2 *>(syms + 2 * (cw * S + s));
     double v[BPS];
-    demap_sym<T, BPS, TDEC_DM_F32OUT>((T)z.x, (T)z.y, cons, c, v);
+    demap_sym<T, BPS, DM_F32OUT>((T)z.x, (T)z.y, cons, c, v);
     float *base = planes + (cw / WAVE) * tile_floats(N);
     const int lane = (int)(cw & (WAVE - 1));
 #pragma unroll
@@ -3327,7 +2609,7 @@ template <typename T, int BPS> struct DemapPro {
                 if (cw >= B || sy >= S) continue;
                 const float2 z = *reinterpret_cast<const float2 *>(a.syms + 2 * (cw * S + sy));
                 double v[BPS];
-                demap_sym<T, BPS, TDEC_DM_F32OUT>((T)z.x, (T)z.y, cons, a.c, v);
+                demap_sym<T, BPS, DM_F32OUT>((T)z.x, (T)z.y, cons, a.c, v);
 #pragma unroll
                 for (int b = 0; b < BPS; ++b) {
                     const long j = sy * BPS + b;
@@ -3362,7 +2644,7 @@ template <typename T, int BPS> struct DemapPro {
 };
 
 template <int ALGO, bool RAG, typename T, int BPS>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ALGO ? TDEC_LM_WPE : TDEC_ML_WPE))) void
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void
 k_turbo_decode_syms(DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv,
                     const int *__restrict__ used, FusedDemapArgs fa) {
     __shared__ uint32_t epi[WAVES_PER_BLOCK * 2 * WAVE];

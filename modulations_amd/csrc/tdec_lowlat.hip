@@ -131,16 +131,13 @@ struct LLIn2 {   // decoder 2: {W2, Y2} and the pre-summed P1[perm[k]] (:511-516
 };
 // The positions whose extrinsic is computed: i -> pos(i), i < count(N).  Before
 // the last iteration decoder 1's output is read only as P1[perm[j]], so only the
-// n_used positions in perm's image (355 of 752) are computed
-// (TDEC_LL_SKIP_UNUSED); otherwise every position.
-#ifndef TDEC_LL_SKIP_UNUSED
-#define TDEC_LL_SKIP_UNUSED 1
-#endif
+// n_used positions in perm's image (355 of 752) are computed; in the last
+// iteration every position.
 struct LLOut1 {  // P1 = f64(Lc) + Le1 for decoder 2, Le1 itself in the last iteration
     double2 *P1, *Le1;
     const lds_int *ulist;   // LDS copy (a per-lane index, as the gathers')
     int n_used;
-    __device__ __forceinline__ bool sparse() const { return TDEC_LL_SKIP_UNUSED && !Le1; }
+    __device__ __forceinline__ bool sparse() const { return !Le1; }
     __device__ __forceinline__ int count(int N) const { return sparse() ? n_used : N; }
     __device__ __forceinline__ int pos(int i) const { return sparse() ? ulist[i] : i; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
@@ -155,23 +152,13 @@ struct LLOut2 {
     __device__ __forceinline__ void store(int k, double a, double b, float, float) const { Le2[k] = make_double2(a, b); }
 };
 
-__device__ __forceinline__ void ll_pm(const float (&g)[8], float (&pm)[8]) {
-    float p2[2][4];
-    pair_max(g, p2);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) pm[i] = p2[i >> 2][i & 3];
-}
-
-// TDEC_LL_SPREAD: the branch metrics spread over the row instead of all 8 in every
-// lane: lane j forms g[j & 7] only (gamma_from_sums's f64 operations for that
+// The branch metrics spread over the row instead of all 8 in every lane: lane j
+// forms g[j & 7] only (gamma_from_sums's f64 operations for that
 // element: the same bits), the pair maxima come from the quad partner by one DPP
 // move (pm[t][wy] pairs g[t*4 + wy] with g[t*4 + 3 - wy], lanes j and j ^ 3), and
 // each lane fetches the two pair maxima (extrinsic: the four metrics) it needs
 // with permutes that do not wait on the recursion, instead of selecting them
 // from 8 registers with cndmask chains.
-#ifndef TDEC_LL_SPREAD
-#define TDEC_LL_SPREAD 1
-#endif
 __device__ __forceinline__ float gamma_lane(double inA, double inB, float w, float y, int i) {
     const double hA = inA * 0.5, hB = inB * 0.5, hW = (double)w * 0.5, hY = (double)y * 0.5;
     const double l1 = hA + (((i >> 2) & 1) ? -hB : hB);
@@ -193,25 +180,8 @@ __device__ __forceinline__ LLRec ll_rec(const SplLane &L, bool beta) {
     return beta ? LLRec{L.sucA, L.sucB, L.pmS0, L.pmS1, L.base} : LLRec{L.srcA, L.srcB, L.pmA, L.pmB, L.base};
 }
 // state 0's value of the lane's 16-lane row: DPP row_newbcast:0 (gfx90a+), no LDS round trip
-#ifndef TDEC_LL_BCAST
-#define TDEC_LL_BCAST 1
-#endif
-__device__ __forceinline__ float row_lane0(float n, int base) {
-    if constexpr (TDEC_LL_BCAST) return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));
-    return __shfl(n, base);
-}
-__device__ __forceinline__ float ll_step(float v, const float (&pm)[8], const LLRec &R) {
-    const float x = __shfl(v, R.src0) + sel8(pm, R.i0);
-    const float y = __shfl(v, R.src1) + sel8(pm, R.i1);
-    const float n = fmaxf(fmaxf(NEG, x), y);
-    return n - row_lane0(n, R.base);
-}
-// the same step with the lane's two pair maxima already fetched
-__device__ __forceinline__ float ll_step2(float v, float p0, float p1, const LLRec &R) {
-    const float x = __shfl(v, R.src0) + p0;
-    const float y = __shfl(v, R.src1) + p1;
-    const float n = fmaxf(fmaxf(NEG, x), y);
-    return n - row_lane0(n, R.base);
+__device__ __forceinline__ float row_lane0(float n, int) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(n), 0x150, 0xF, 0xF, false));
 }
 template <class In> __device__ __forceinline__ void lane_pms(const In &in, const LLRaw &r, int s, const LLRec &R,
                                                             float &p0, float &p1) {
@@ -223,9 +193,6 @@ template <class In> __device__ __forceinline__ void lane_pms(const In &in, const
 }
 
 constexpr int LL_D = 8;   // loads issued this many steps ahead of their use
-#ifndef TDEC_LL_PIPE
-#define TDEC_LL_PIPE 1
-#endif
 
 // One SISO (:116-281) of the wave's codeword.  ast / bst: stores [N + 1][16]
 // (lane s: element s); ast[k] = alpha2[k], bst[k] = beta2[k] on exit.
@@ -243,7 +210,7 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
         auto slot = [&](int k) { return (beta ? N - k : k) * 16 + s; };
         LLRaw r[LL_D];
         float v = 0.0f;
-        if constexpr (TDEC_LL_PIPE) {
+        {
             // Software-pipelined: the next step's pair maxima (gamma's f64 chain and
             // two permutes) are formed while this step's neighbour permutes are in
             // flight, and the gather indices of the group after next are read from
@@ -305,67 +272,8 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
                     }
                 }
             }
-        } else {
-        float g[8], pm[8];
-        double iA, iB;
-        // pass 1 from 0, every vector stored
-#pragma unroll
-        for (int j = 0; j < LL_D; ++j) r[j] = in.load(pos(min(j, N - 1)));
-        for (int k0 = 0; k0 < N; k0 += LL_D) {
-#pragma unroll
-            for (int j = 0; j < LL_D; ++j) {
-                const int k = k0 + j;
-                if (k >= N) break;   // uniform
-                if constexpr (TDEC_LL_SPREAD) {
-                    float p0, p1;
-                    lane_pms(in, r[j], s, R, p0, p1);
-                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                    vst[slot(k)] = v;
-                    v = ll_step2(v, p0, p1, R);
-                } else {
-                    in.gamma(r[j], g, iA, iB);
-                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                    ll_pm(g, pm);
-                    vst[slot(k)] = v;
-                    v = ll_step(v, pm, R);
-                }
-            }
-        }
-        // pass 2 from alpha1[N] / beta1[0] until the group's vector equals the stored one
-        bool merged = false;
-#pragma unroll
-        for (int j = 0; j < LL_D; ++j) r[j] = in.load(pos(min(j, N - 1)));
-        for (int k0 = 0; k0 < N; k0 += LL_D) {
-            if (__all(merged || grp >= 2)) break;
-            float c[LL_D];
-#pragma unroll
-            for (int j = 0; j < LL_D; ++j) c[j] = vst[slot(min(k0 + j, N - 1))];
-#pragma unroll
-            for (int j = 0; j < LL_D; ++j) {
-                const int k = k0 + j;
-                if (k >= N) break;
-                if (!merged) merged = group_all(v == c[j], L.base);
-                if constexpr (TDEC_LL_SPREAD) {
-                    float p0, p1;
-                    lane_pms(in, r[j], s, R, p0, p1);
-                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                    if (!merged) {
-                        vst[slot(k)] = v;
-                        v = ll_step2(v, p0, p1, R);
-                    }
-                } else {
-                    in.gamma(r[j], g, iA, iB);
-                    r[j] = in.load(pos(min(k + LL_D, N - 1)));
-                    if (!merged) {
-                        ll_pm(g, pm);
-                        vst[slot(k)] = v;
-                        v = ll_step(v, pm, R);
-                    }
-                }
-            }
         }
     }
-        }
     ll_sync();
     // extrinsic (:232-281) from the stored alpha2[k], beta2[k+1] at every position
     // anyone reads (out.pos(i), i < M): group q takes i = q, q + 4, ...
@@ -388,19 +296,13 @@ __device__ void ll_siso(const In &in, const Out &out, int N, float *ast, float *
         for (int j = 0; j < LL_D; ++j) {
             const int i = i0 + 4 * j, k = kk[j];
             if (!__any(i < M)) break;   // the groups run different i: wave-level exit
-            float g[8];
             double iA, iB;
-            float gl = 0.0f;
-            if constexpr (TDEC_LL_SPREAD) {
-                in.sums(r[j], iA, iB);
-                gl = gamma_lane(iA, iB, r[j].v.z, r[j].v.w, s & 7);
-            } else {
-                in.gamma(r[j], g, iA, iB);
-            }
+            in.sums(r[j], iA, iB);
+            const float gl = gamma_lane(iA, iB, r[j].v.z, r[j].v.w, s & 7);
             float app[4];
 #pragma unroll
             for (int inp = 0; inp < 4; ++inp) {
-                const float gv = TDEC_LL_SPREAD ? __shfl(gl, L.base + L.gi[inp]) : sel8(g, L.gi[inp]);
+                const float gv = __shfl(gl, L.base + L.gi[inp]);
                 const float t = (av[j] + (L.gn[inp] ? -gv : gv)) + ((inp == 0 || inp == 3) ? bx[j] : by[j]);
                 app[inp] = fmaxf(NEG, t);
             }

@@ -437,18 +437,25 @@ def _siso_inputs(Lc, La, N, ndim):
         run the float64 one, where those sums are formed from the unrounded
         values.  Widening is exact, so a float32 array in a mixed call gives the
         values numba uses.
-      * a-priori: float64 only.  With float32 La the reference sums in_A = Lc_A +
-        La_A in float32 and builds the branch metrics from a float32 m, which the
-        shim that pins every fixture cannot reproduce (numpy 2 keeps 0.0 + f32 in
+      * a-priori: float64, or integer / bool arrays, which numba widens to f64
+        exactly as integer channel LLRs (int64 + f64 -> f64): they are widened
+        here.  With float32 (or float16) La the reference sums in_A = Lc_A + La_A
+        in float32 and builds the branch metrics from a float32 m, which the shim
+        that pins every fixture cannot reproduce (numpy 2 keeps 0.0 + f32 in
         float32 where numba promotes to f64), so that call is refused, not guessed.
-    Returns (f64, [A, B, W, Y], [LaA, LaB]): the caller's arrays (not copied),
-    each checked to be ndim-D with at least N entries along its last axis."""
+    Returns (f64, [A, B, W, Y], [LaA, LaB]): the caller's arrays (not copied;
+    integer a-priori arrays widened to float64), each checked to be ndim-D with at
+    least N entries along its last axis."""
     lc = [x if type(x) is np.ndarray else np.asarray(x) for x in Lc]
     la = [x if type(x) is np.ndarray else np.asarray(x) for x in La]
-    for x in la:
-        if x.dtype is not _F64 and x.dtype != _F64:
-            raise TypeError(f"bcjr_max_log_map: a-priori LLRs must be float64 (got {x.dtype}); the reference's "
-                            "float32 a-priori arithmetic is not reproducible here (parity unpinned)")
+    for i, x in enumerate(la):
+        if x.dtype is _F64 or x.dtype == _F64:
+            continue
+        if x.dtype.kind in "iub" and x.dtype.itemsize <= 8:
+            la[i] = x.astype(np.float64)   # exact for |v| < 2^53, as numba's int64 -> f64
+            continue
+        raise TypeError(f"bcjr_max_log_map: a-priori LLRs must be float64 or integer (got {x.dtype}); the "
+                        "reference's float32 a-priori arithmetic is not reproducible here (parity unpinned)")
     f64 = False
     for x in lc:
         if x.dtype is not _F32 and x.dtype != _F32:
@@ -480,6 +487,10 @@ def bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, 
     if N == 0:   # the reference's recursions run over range(0): empty extrinsics
         return np.zeros(0), np.zeros(0)
     h = _siso_handle(N, _tables_key((next_st, out_W, out_Y, prev_st, prev_inp)), 0, _default_device())
+    if h.siso_staged is None:   # a library without the staged entry points (older A/B builds)
+        LeA, LeB = bcjr_max_log_map_batch(*(x[None, :N] for x in lc + la), next_st, out_W, out_Y, prev_st, prev_inp,
+                                          N, scaling_factor)
+        return LeA[0], LeB[0]
     v = h.siso_views()[f64]
     with h.lock:
         for d, x in zip(v, lc + la):
@@ -491,6 +502,19 @@ def bcjr_max_log_map(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, 
 
 
 bcjr_decode_circular = bcjr_max_log_map   # historic name of the same SISO
+
+
+def siso_flag_fallbacks():
+    """Staged bcjr_max_log_map calls, over every cached SISO handle, that ended by
+    a stream wait instead of their rows' completion flags (tdec_siso_stats; 0 when
+    the flag path works)."""
+    n = 0
+    L = _n.lib()
+    for h in list(_SISO_CACHE.values()):
+        v = C.c_long(0)
+        _n.check(L.tdec_siso_stats(h.h, C.byref(v)))
+        n += v.value
+    return n
 
 
 def bcjr_max_log_map_batch(Lc_A, Lc_B, Lc_W, Lc_Y, La_A, La_B, next_st, out_W, out_Y, prev_st, prev_inp, N,

@@ -28,10 +28,18 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _oracle(codec, llr, algo=1):
+def _oracle(codec, llr, algo=1, want_lfinal=False):
     t, _ = O.trellis()
     return O.decode_batch(llr, codec.N, codec.punct["period"], T.puncture_matrix(codec.punct), codec.iterations,
-                          codec.perm, codec.inv_perm, t, algo=algo, nthreads=8)
+                          codec.perm, codec.inv_perm, t, algo=algo, nthreads=16, want_lfinal=want_lfinal)
+
+
+def _rows(B, n_first, n_spread):
+    """The first n_first rows and n_spread spread over the rest, the last included."""
+    idx = np.unique(np.concatenate([np.arange(min(B, n_first)),
+                                    np.linspace(min(B, n_first), B - 1, n_spread).astype(np.int64)]))
+    assert idx[-1] == B - 1
+    return idx
 
 
 def _host_llrs(codec, syms_rows, mod, n0):
@@ -41,20 +49,24 @@ def _host_llrs(codec, syms_rows, mod, n0):
     return np.stack([-O.demap(r, cons, bps, nve, div_f32=div32)[:codec.n_coded] for r in syms_rows]).astype(np.float32)
 
 
-def test_8psk_demap_planes_to_logmap_decode_n752_r12():
+@pytest.mark.parametrize("B", [96, 7232])
+def test_8psk_demap_planes_to_logmap_decode_n752_r12(B):
+    """B = 96: the frame decoder (small batches); B = 7 232 > LM_FRAME_MAX (7 168):
+    the timed throughput kernel k_turbo_decode_logmap."""
     dev = torch.device("cuda", 0)
     codec = M.DVBRCS2_Turbo(752, "1/2", algo="log-map")
     assert codec.n_coded == 3008
-    B = 96
     info, syms, n0 = make_symbols(codec, B, "8PSK", 3.0, 11, dev)
     assert syms.shape == (B, 1003)                        # 3008 bits + 1 zero pad bit -> 1003 symbols
     pipe = DevicePipeline(codec, "8PSK", B, dev)
     bits = pipe.run(syms, n0).clone()
     torch.cuda.synchronize()
-    llr = _host_llrs(codec, syms.cpu().numpy(), "8PSK", n0)
-    assert np.array_equal(bits.cpu().numpy(), _oracle(codec, llr))
+    idx = _rows(B, 256, 256) if B > 96 else np.arange(B)
+    llr = _host_llrs(codec, syms[torch.as_tensor(idx, device=dev)].cpu().numpy(), "8PSK", n0)
+    assert np.array_equal(bits[torch.as_tensor(idx, device=dev)].cpu().numpy(), _oracle(codec, llr))
     # and through the LLR-row boundary (host demap -> f32 -> decode): the same bits
-    assert np.array_equal(codec.decode_batch(llr), bits.cpu().numpy())
+    if B == 96:
+        assert np.array_equal(codec.decode_batch(llr), bits.cpu().numpy())
 
 
 def test_logmap_full_size_tile_wrap():
@@ -77,6 +89,32 @@ def test_logmap_full_size_tile_wrap():
     idx = [0, 1, 63, 64, 131_071, 131_072, B // 2, B - 65, B - 1]
     llr = _host_llrs(codec, syms[idx].cpu().numpy(), "8PSK", n0)
     assert np.array_equal(b1[idx].cpu().numpy(), _oracle(codec, llr))
+
+
+def test_logmap_timed_kernel_vs_oracle_4096_rows():
+    """The timed kernel itself (k_turbo_decode_logmap, configs[3]'s shape) against
+    the oracle on 4 096 rows of a 140 000-codeword batch: the
+    first 2 048 (32 tiles of the first round) and 2 048 spread over the batch, the
+    ragged last tile and rows of every round of the persistent loop included; bits
+    AND L_final, IEEE ==.  (~30 s of 16-thread oracle time.)"""
+    dev = torch.device("cuda", 0)
+    codec = M.DVBRCS2_Turbo(752, "1/2", algo="log-map")
+    B = 140_000
+    info, syms, n0 = make_symbols(codec, B, "8PSK", 3.0, 5, dev)
+    pipe = DevicePipeline(codec, "8PSK", B, dev)
+    b1 = pipe.run(syms, n0).clone()
+    lf = torch.empty((B, codec.k_info), dtype=torch.float64, device=dev)
+    bits = torch.empty((B, codec.k_info), dtype=torch.int32, device=dev)
+    codec.decode_planes_device(pipe.planes, B, bits, lfinal=lf)
+    torch.cuda.synchronize()
+    assert torch.equal(bits, b1)
+    idx = _rows(B, 2048, 2048)
+    assert len(idx) >= 4096
+    ti = torch.as_tensor(idx, device=dev)
+    llr = _host_llrs(codec, syms[ti].cpu().numpy(), "8PSK", n0)
+    rb, rl = _oracle(codec, llr, want_lfinal=True)
+    assert np.array_equal(bits[ti].cpu().numpy(), rb)
+    np.testing.assert_array_equal(lf[ti].cpu().numpy(), rl)
 
 
 # ---- the hardware primitives of the build-defined log-MAP (DESIGN.md §2) -------------

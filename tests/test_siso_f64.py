@@ -89,7 +89,7 @@ def test_widened_f32_equals_f32_specialisation(G_siso, n):
         _eq(b, g[f"LeB_{n}"][j])
 
 
-@pytest.mark.parametrize("bad", ["la_f32", "la_int", "lc_f16", "lc_complex", "lc_object", "la_f32_batch"])
+@pytest.mark.parametrize("bad", ["la_f32", "la_f16", "lc_f16", "lc_complex", "lc_object", "la_f32_batch"])
 def test_unpinnable_dtypes_raise(bad):
     n = 48
     rng = np.random.default_rng(1)
@@ -97,8 +97,8 @@ def test_unpinnable_dtypes_raise(bad):
     La = [rng.standard_normal(n) for _ in range(2)]
     if bad.startswith("la_f32"):
         La[0] = La[0].astype(np.float32)
-    elif bad == "la_int":
-        La[1] = np.arange(n)
+    elif bad == "la_f16":
+        La[1] = La[1].astype(np.float16)
     elif bad == "lc_f16":
         Lc[2] = Lc[2].astype(np.float16)
     elif bad == "lc_complex":
@@ -110,6 +110,17 @@ def test_unpinnable_dtypes_raise(bad):
             M.bcjr_max_log_map_batch(*(x[None] for x in Lc), *(x[None] for x in La), *TABLES, n, 0.7)
         else:
             M.bcjr_max_log_map(*Lc, *La, *TABLES, n, 0.7)
+
+
+def test_integer_a_priori_widens_to_float64():
+    """Integer / bool a-priori arrays are widened to float64, as numba widens
+    int64 + f64: the same inputs the f64 specialisation sees."""
+    n = 48
+    Lc = [np.zeros(n, np.float32) for _ in range(4)]
+    f64, lc, la = M._siso_inputs(Lc, (np.arange(n), np.ones(n, bool)), n, 1)
+    assert not f64
+    assert all(x.dtype == np.float64 for x in la)
+    assert np.array_equal(la[0], np.arange(n, dtype=np.float64)) and np.array_equal(la[1], np.ones(n))
 
 
 def test_short_and_misshapen_inputs_raise():
@@ -215,3 +226,26 @@ def test_gpu_logmap_f64_rows_vs_oracle(n):
         ra, rb = O.siso(*(x[r] for x in Lc), *(x[r] for x in La), TAB, 0.7, algo=1)
         _eq(a[r], ra)
         _eq(b[r], rb)
+
+
+@pytest.mark.gpu
+def test_gpu_integer_a_priori_and_flag_path():
+    """Integer a-priori arrays give the float64 call's extrinsics bit for bit
+    (numba's int64 -> f64 widening), and every staged single call of
+    this session ended on its completion flags, never on the time-limited
+    fallback stream wait (tdec_siso_stats)."""
+    _gpu()
+    rng = np.random.default_rng(5)
+    for n in (48, 212, 752):
+        Lc = [(rng.standard_normal(n) * 3).astype(np.float32) for _ in range(4)]
+        La = [rng.integers(-20, 21, n), rng.integers(-20, 21, n).astype(np.int32)]
+        a, b = M.bcjr_max_log_map(*Lc, *La, *TABLES, n, 0.7)
+        ra, rb = M.bcjr_max_log_map(*Lc, *(x.astype(np.float64) for x in La), *TABLES, n, 0.7)
+        _eq(a, ra)
+        _eq(b, rb)
+        oa, ob = O.siso(*Lc, *(x.astype(np.float64) for x in La), TAB, 0.7)
+        _eq(a, oa)
+        _eq(b, ob)
+    for _ in range(200):   # a burst of single calls: each must complete on its flags
+        M.bcjr_max_log_map(*Lc, *(x.astype(np.float64) for x in La), *TABLES, 752, 1.0)
+    assert M.siso_flag_fallbacks() == 0

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-wave placement and duration of one tile-decoder launch (measurement
 builds with TDEC_WAVE_TIMING=1): decodes one batch with each given library,
-the library appends (wave, start, end, tiles, HW_ID, XCC_ID) rows to
-$TDEC_WAVE_DUMP at tdec_destroy; then summarises waves per CU / per SIMD
-against wave duration.
+the library appends (wave, start, end, tiles, HW_ID, XCC_ID, shader-clock start,
+end) rows to $TDEC_WAVE_DUMP at tdec_destroy; then summarises waves per CU / per
+SIMD against wave duration, and the shader clock the waves ran at (s_memtime
+ticks over s_memrealtime's 100 MHz: the DVFS state under this kernel).
 
   TDEC_WAVE_DUMP=out.txt python tools/wave_dump.py lib_a.so [lib_b.so] --n 212 --mod QPSK --batch 102400
 """
@@ -41,7 +42,7 @@ def decode(libs, a):
         L = C.CDLL(os.path.abspath(p))
         _native._declare(L)
         h = C.c_void_p()
-        assert L.tdec_create(0, a.n, codec.punct["period"], pm.ctypes.data, 8, 0, codec.perm.ctypes.data,
+        assert L.tdec_create(0, a.n, codec.punct["period"], pm.ctypes.data, 8, a.algo, codec.perm.ctypes.data,
                              codec.inv_perm.ctypes.data, tabs.ctypes.data, C.byref(h)) == 0
         assert L.tdec_reserve(h, B) == 0
         for _ in range(2):   # the dump keeps the last launch
@@ -83,6 +84,10 @@ def summarise(path, libs, waves):
             by[(per_cu[key_cu(r)], per_simd[key_simd(r)])].append(dur[r[0]])
         print("  (waves on CU, waves on SIMD) -> mean ms:",
               ", ".join(f"{k}: {np.mean(v):.2f} (n={len(v)})" for k, v in sorted(by.items())))
+        if all(len(r) >= 8 for r in rows):
+            ghz = np.array([(r[7] - r[6]) / max(1.0, (r[2] - r[1]) * 10.0) for r in rows])
+            print(f"  shader clock per wave: mean {ghz.mean():.3f} GHz, p10 {np.percentile(ghz, 10):.3f}, "
+                  f"p90 {np.percentile(ghz, 90):.3f}, min {ghz.min():.3f}, max {ghz.max():.3f}")
 
 
 def main():
@@ -92,6 +97,7 @@ def main():
     ap.add_argument("--n", type=int, default=212)
     ap.add_argument("--rate", default="1/3")
     ap.add_argument("--mod", default="QPSK")
+    ap.add_argument("--algo", type=int, default=0)
     a = ap.parse_args()
     path = os.environ["TDEC_WAVE_DUMP"]
     if os.path.exists(path):

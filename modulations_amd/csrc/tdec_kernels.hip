@@ -474,15 +474,22 @@ struct LdsStage {
 // zero row read with row stride 0 (L2-resident), so the loads are the same
 // straight-line code in every iteration: no branch for the compiler's
 // wait-count analysis to merge pessimistically.
-struct TileIn {
+// SUB (sub-tiles, see turbo_decode_tiles): the wave's codewords are a range of T <
+// 64 that can straddle two plane tiles, so the planes are addressed by a virtual
+// lane xl (float4 units from the first tile's base) while the workspace keeps the
+// hardware lane.
+template <bool SUB = false> struct TileIn {
     const float4 *X;
     const double2 *La;
     const int *la_idx;
     int lane;
     unsigned rs;   // workspace row stride (elements between trellis steps)
+    int xl = 0;    // SUB: the lane's plane offset
+    static constexpr bool SUBT = SUB;
+    __device__ __forceinline__ int xlane() const { return SUB ? xl : lane; }
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
-        r.v = at(X, k * WAVE + lane);
+        r.v = at(X, k * WAVE + xlane());
         r.l = at(La, wsrow(la_idx[k], rs) + lane);
         return r;
     }
@@ -490,7 +497,7 @@ struct TileIn {
         make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
-        glds16s(X, (unsigned)(k * WAVE + lane) * 16u, st.v + j * WAVE);
+        glds16s(X, (unsigned)(k * WAVE + xlane()) * 16u, st.v + j * WAVE);
         glds16s(La, (wsrow(la_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
@@ -506,15 +513,18 @@ struct TileIn {
 // Decoder 2: the sums inA = f64(Lc_A[perm[k]]) + Le1_A[perm[k]] (:511-516)
 // gathered from decoder 1's pre-summed output P1 (P1[j] = f64(Lc_A[j]) +
 // Le1_A[j], the same f64 addition), parities from Z = [N][64] float2 {W2, Y2}.
-struct TileInPre {
+template <bool SUB = false> struct TileInPre {
     const float2 *Z;
     const double2 *P;
     const int *p_idx;
     int lane;
     unsigned rs;
+    int xl = 0;    // SUB: the lane's plane offset (float2 units)
+    static constexpr bool SUBT = SUB;
+    __device__ __forceinline__ int xlane() const { return SUB ? xl : lane; }
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
-        const float2 z = at(Z, k * WAVE + lane);
+        const float2 z = at(Z, k * WAVE + xlane());
         r.v = make_float4(0.0f, 0.0f, z.x, z.y);
         r.l = at(P, wsrow(p_idx[k], rs) + lane);
         return r;
@@ -527,7 +537,7 @@ struct TileInPre {
     // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         lds_f1 *dst = reinterpret_cast<lds_f1 *>(st.v + j * WAVE);
-        const unsigned zo = (unsigned)(k * WAVE + lane) * 8u;
+        const unsigned zo = (unsigned)(k * WAVE + xlane()) * 8u;
         glds4s(Z, zo, dst);
         glds4s(Z, zo + 4u, dst + WAVE);
         glds16s(P, (wsrow(p_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
@@ -1209,6 +1219,7 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         In inp = in;
         int lanep = lane;
         asm volatile("" : "+v"(inp.lane), "+v"(lanep));
+        if constexpr (In::SUBT) asm volatile("" : "+v"(inp.xl));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             raw[j] = inp.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
@@ -1325,6 +1336,7 @@ struct DecodeArgs {
     // graph keeps its tail_seq, so on replay the gate finds the flag already raised.
     unsigned *tail_flag = nullptr;
     unsigned tail_seq = 0;
+    int unit_cw = WAVE;      // codewords per work unit (64, or T < 64 with sub-tiles)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1357,7 +1369,15 @@ __device__ int g_wave_tiles[WT_MAX];
 __device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of each wave
 #endif
 
-template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
+// Work units.  Normally a unit is one 64-codeword plane tile (unit_cw = 64).  SUB
+// (sub-tiles): a batch of less than one round of resident waves x 64 codewords gives
+// every resident wave one unit of T = ceil(B / waves) < 64 codewords, so every
+// SIMD holds two equally loaded waves instead of some two full ones and some one
+// (configs[1]: 1 600 tiles on 2 048 wave slots).  A unit's
+// codewords [u T, u T + T) may straddle two plane tiles: each lane addresses the
+// planes by a virtual lane from the first tile's base (idle lanes >= T mirror the
+// unit's last codeword and write nothing).
+template <int ALGO, bool RAG, bool STAGED = false, bool SUB = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, const int *__restrict__ used,
                                                    float4 *lv, double2 *ll,
@@ -1413,19 +1433,32 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             if (p.tail_flag && lane == 0 && (p.tile_ctr ? !has_next : tile == p.n_tiles - 1))
                 atomicMax(p.tail_flag, p.tail_seq);
         }
-        const float *base = pro.tile_planes(tile, wave, N, buf);
+        const int T = SUB ? p.unit_cw : WAVE;
+        const long c0 = (long)tile * T;                 // the unit's first codeword
+        int xl = lane, zl = lane;
+        const float *base;
+        if constexpr (SUB) {
+            const long t0 = c0 >> 6;
+            const long cl = min(c0 + min(lane, T - 1), (long)p.B - 1);   // inside the planes' tiles
+            const int dt = (int)((cl >> 6) - t0);
+            xl = (int)(cl & 63) + dt * N * 96;        // float4s per plane tile: N * 64 * 6 / 4
+            zl = (int)(cl & 63) + dt * N * 192;       // float2s per plane tile
+            base = pro.tile_planes((int)t0, wave, N, buf);
+        } else {
+            base = pro.tile_planes(tile, wave, N, buf);
+        }
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
         {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
+            run_siso<ALGO, RAG, STAGED>(TileIn<SUB>{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u, xl},
                                         TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs,
                                         lane, sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
-            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
-                                        sf, lv, ll, pr);
+            run_siso<ALGO, RAG, STAGED>(TileInPre<SUB>{Z, P1, perm, lane, rs, zl}, TileOut{Le2, lane, rs}, N, ck, ring,
+                                        rs, lane, sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
@@ -1439,12 +1472,13 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         // writes the 64 rows chunk by chunk in row order (16-B int4 stores, each
         // wave store one contiguous 1 KiB run) instead of one 8-B store per lane
         // per couple 6 KB apart.
-        const long cw = (long)tile * WAVE + lane;
+        const long cw = c0 + lane;
+        const bool lane_on = lane < T && cw < p.B;
         uint32_t *hb = epi + (threadIdx.x >> 6) * epi_stride;
         const long nb = 2L * N;
         for (int kc = 0; kc < N; kc += 32) {
             uint32_t w0 = 0, w1 = 0;
-            double *lo = (p.lfinal && cw < p.B) ? p.lfinal + cw * nb : nullptr;
+            double *lo = (p.lfinal && lane_on) ? p.lfinal + cw * nb : nullptr;
             const int kn = min(32, N - kc);
             // groups of 8 steps whose 24 loads are issued together (one exposed
             // memory latency per group, not per step; 3.2 % of the decode before)
@@ -1454,7 +1488,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int k = min(kc + kg + u, N - 1);   // past the chunk: a valid row, unused
-                    const float4 x = at(X, k * WAVE + lane);
+                    const float4 x = at(X, k * WAVE + xl);
                     xa[u] = make_float2(x.x, x.y);
                     la[u] = at(Le2, wsrow(inv[k], rs) + lane);
                     le[u] = at(Le1, wsrow(k, rs) + lane);
@@ -1480,8 +1514,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             const int per = (2 * kn + 3) / 4;
             for (int t = lane; t < WAVE * per; t += WAVE) {
                 const int l = t / per, pc = t - l * per;
-                const long row = (long)tile * WAVE + l;
-                if (row >= p.B) continue;
+                const long row = c0 + l;
+                if (l >= T || row >= p.B) continue;
                 const uint32_t w = hb[(pc >> 3) * WAVE + l] >> (4 * (pc & 7));
                 const int j = 4 * pc;                          // first int32 of the piece within the chunk
                 int32_t *dst = p.bits + row * nb + 2L * kc + j;
@@ -1531,6 +1565,15 @@ __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_W
     __shared__ double2 ll[LDS_STAGE];
     turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
                                      EPI_STRIDE_ML);
+}
+// The same decoder over sub-tile work units (turbo_decode_tiles, SUB).
+template <bool RAG>
+__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_sub(
+    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
+    __shared__ float4 lv[LDS_LV];
+    __shared__ double2 ll[LDS_STAGE];
+    turbo_decode_tiles<0, RAG, true, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv),
+                                           PlanesIn{p.planes}, EPI_STRIDE_ML);
 }
 template <bool RAG>
 __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_logmap(

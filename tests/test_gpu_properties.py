@@ -151,3 +151,19 @@ def test_ragged_checkpoint_windows_full_size(n, mod):
     assert torch.equal(b1, b2)
     # the timed kernel against the oracle: 4 096 rows (incl. the last, ragged tile), bits and L_final
     assert torch.equal(_check_throughput_kernel_vs_oracle(codec, pipe, syms, B, n0, mod), b1)
+
+
+@pytest.mark.parametrize("n,mod,B", [(212, "QPSK", 102_400), (220, "16QAM", 100_003), (752, "16QAM", 70_001)])
+def test_sub_tile_units_vs_oracle(n, mod, B):
+    """Batches of more 64-codeword tiles than SIMDs but fewer than resident waves
+    run sub-tile units (every resident wave one unit of ceil(B / waves) < 64
+    codewords): configs[1]'s shape, a ragged N whose units
+    straddle plane tiles and end in a partial unit, and N = 752 -- 4 096 rows
+    against the oracle, bits and L_final, and deterministic."""
+    dev = torch.device("cuda", 0)
+    codec = M.DVBRCS2_Turbo(n, "1/3")
+    _, syms, n0 = make_symbols(codec, B, mod, 1.5, 23, dev, want_info=False)
+    pipe = DevicePipeline(codec, mod, B, dev)
+    b1 = pipe.run(syms, n0).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(_check_throughput_kernel_vs_oracle(codec, pipe, syms, B, n0, mod), b1)

@@ -55,7 +55,9 @@ def summarise(path, libs, waves):
     blocks = open(path).read().split("# launch")[1:]
     for lib, blk in zip(libs, blocks):
         rows = [list(map(int, l.split())) for l in blk.strip().splitlines()[1:]]
-        rows = [r for r in rows if r[0] < waves and r[2] > 0]
+        rows = [r for r in rows if r[2] > 0]
+        s_last = max(r[1] for r in rows)   # the last launch's waves start within ~0.1 ms of each other
+        rows = [r for r in rows if r[1] >= s_last - 50000]
         t0 = min(r[1] for r in rows)
         dur = {r[0]: (r[2] - r[1]) * 1e-5 for r in rows}
         end = {r[0]: (r[2] - t0) * 1e-5 for r in rows}

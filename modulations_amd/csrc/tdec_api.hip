@@ -335,8 +335,7 @@ int check_demap_args(int M, int bps) {
 
 typedef void (*decode_fn)(DecodeArgs, const int *, const int *, const int *);
 
-const void *decode_kernel(int algo, bool ragged, bool sub = false) {
-    if (sub) return ragged ? (const void *)k_turbo_decode_sub<true> : (const void *)k_turbo_decode_sub<false>;
+const void *decode_kernel(int algo, bool ragged) {
     if (algo) return ragged ? (const void *)k_turbo_decode_logmap<true> : (const void *)k_turbo_decode_logmap<false>;
     return ragged ? (const void *)k_turbo_decode<true> : (const void *)k_turbo_decode<false>;
 }
@@ -853,27 +852,6 @@ static int ensure_ws(tdec_t *h, int waves) {
     return 0;
 }
 
-// Work units of the throughput decoder (turbo_decode_tiles): 64-codeword tiles,
-// or -- a max-log batch of more tiles than SIMDs but fewer than resident waves
-// (some SIMDs would hold two waves, some one) -- one unit of T = ceil(B / waves)
-// codewords per resident wave, so every SIMD holds two equally loaded waves.
-// Returns the waves the launch runs; *unit_cw = codewords per unit.
-#ifndef TDEC_SUB_TILES
-#define TDEC_SUB_TILES 1   // A/B switch (round 6)
-#endif
-static int decode_units(const tdec_t *h, int B, int *unit_cw, int *units) {
-    const int tiles = n_tiles_of(B);
-    if (TDEC_SUB_TILES && h->algo == TDEC_ALGO_MAXLOG && 2 * tiles > h->max_waves && tiles < h->max_waves) {
-        const int T = (B + h->max_waves - 1) / h->max_waves;
-        *unit_cw = T;
-        *units = (B + T - 1) / T;
-        return *units;
-    }
-    *unit_cw = WAVE;
-    *units = tiles;
-    return std::min(tiles, h->max_waves);
-}
-
 // Batches of at most lowlat_max() codewords (max-log) run the one-codeword-per-
 // wave decoder (tdec_lowlat.hip): lower latency per call.  Measured (N=752 r=1/2,
 // host-pointer call, profiles/r03h_latency.jsonl, r03i_latency_lowlat4096.json):
@@ -1014,8 +992,7 @@ int tdec_reserve(tdec_t *h, int max_batch) {
         if (!rc) h->cap_batch = std::max(h->cap_batch, max_batch);
         return rc;
     }
-    int ucw, nu;
-    const int want_waves = std::max(decode_units(h, max_batch, &ucw, &nu), std::min(n_tiles_of(max_batch), h->max_waves));
+    const int want_waves = std::min(n_tiles_of(max_batch), h->max_waves);
     if (want_waves > h->ws_waves || tdec_planes_bytes(h, max_batch) > h->planes_own.cap ||
         n_tiles_of(max_batch) > h->decl_tiles)
         quiesce(h);   // regrowth frees
@@ -1070,20 +1047,19 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
         HIPCHK(hipGetLastError());
         return mark_used(h, st);
     }
-    int unit_cw, tiles;
-    const int waves = decode_units(h, B, &unit_cw, &tiles);
+    const int tiles = n_tiles_of(B);
+    const int waves = std::min(tiles, h->max_waves);
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
     if (int rc = order_on(h, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used,
                  h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
-    a.unit_cw = unit_cw;
     if (h->d_simd_prog && hipMemsetAsync(h->d_simd_prog, 0, SIMD_PROG_BYTES, st) == hipSuccess) a.simd_prog = h->d_simd_prog;
     a.tail_flag = h->d_tail;
     a.tail_seq = ++h->tail_seq;
     const int *pm = h->d_perm, *iv = h->d_inv;
     const dim3 grid((waves + DEC_WAVES - 1) / DEC_WAVES);
-    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0, unit_cw != WAVE), grid,
-                       dim3(DEC_BLOCK), 0, st, a, pm, iv, (const int *)h->d_used);
+    hipLaunchKernelGGL((decode_fn)decode_kernel(h->algo, h->N % win_of(h->algo) != 0), grid, dim3(DEC_BLOCK), 0, st,
+                       a, pm, iv, (const int *)h->d_used);
     HIPCHK(hipGetLastError());
     return mark_used(h, st);
 }

@@ -128,7 +128,31 @@ __device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two IEEE f32 ops per lane
 
+// TDEC_LM_LUT (round-6 timing experiment, DIFFERENT BITS): the
+// correction log2(1 + 2^-d) from an LDS table of {value, slope} on a 1/256 grid of
+// d in [0, 24) (48 KiB, filled by k_turbo_decode_logmap), linear interpolation:
+// d * 256, cvt, min, fract, ds_read_b64, fma instead of the two transcendentals.
+#ifndef TDEC_LM_LUT
+#define TDEC_LM_LUT 0
+#endif
+#if TDEC_LM_LUT
+constexpr int LM_LUT_N = 24 * 256;
+__shared__ float2 g_lm_lut[LM_LUT_N];
+__device__ void lm_lut_fill() {
+    for (int i = threadIdx.x; i < LM_LUT_N; i += blockDim.x) {
+        const float v0 = hw_log2(1.0f + hw_exp2(-(float)i / 256.0f)), v1 = hw_log2(1.0f + hw_exp2(-(float)(i + 1) / 256.0f));
+        g_lm_lut[i] = make_float2(v0, v1 - v0);
+    }
+    __syncthreads();
+}
+#endif
 __device__ __forceinline__ float jac(float a, float b) {
+#if TDEC_LM_LUT
+    const float x = fabsf(a - b) * 256.0f;
+    const unsigned i = min((unsigned)x, (unsigned)(LM_LUT_N - 1));
+    const float2 e = g_lm_lut[i];
+    return fmaxf(a, b) + fmaf(e.y, __builtin_amdgcn_fractf(x), e.x);
+#endif
     const float t = fabsf(a - b) + LM_C;
     const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
     return fmaxf(a, b) + hw_log2(w);
@@ -474,22 +498,15 @@ struct LdsStage {
 // zero row read with row stride 0 (L2-resident), so the loads are the same
 // straight-line code in every iteration: no branch for the compiler's
 // wait-count analysis to merge pessimistically.
-// SUB (sub-tiles, see turbo_decode_tiles): the wave's codewords are a range of T <
-// 64 that can straddle two plane tiles, so the planes are addressed by a virtual
-// lane xl (float4 units from the first tile's base) while the workspace keeps the
-// hardware lane.
-template <bool SUB = false> struct TileIn {
+struct TileIn {
     const float4 *X;
     const double2 *La;
     const int *la_idx;
     int lane;
     unsigned rs;   // workspace row stride (elements between trellis steps)
-    int xl = 0;    // SUB: the lane's plane offset
-    static constexpr bool SUBT = SUB;
-    __device__ __forceinline__ int xlane() const { return SUB ? xl : lane; }
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
-        r.v = at(X, k * WAVE + xlane());
+        r.v = at(X, k * WAVE + lane);
         r.l = at(La, wsrow(la_idx[k], rs) + lane);
         return r;
     }
@@ -497,7 +514,7 @@ template <bool SUB = false> struct TileIn {
         make_gamma<ALGO>(r.v.x, r.v.y, r.l.x, r.l.y, r.v.z, r.v.w, g, iA, iB);
     }
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
-        glds16s(X, (unsigned)(k * WAVE + xlane()) * 16u, st.v + j * WAVE);
+        glds16s(X, (unsigned)(k * WAVE + lane) * 16u, st.v + j * WAVE);
         glds16s(La, (wsrow(la_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
     }
     __device__ __forceinline__ Raw staged(const LdsStage &st, int j) const {
@@ -513,18 +530,15 @@ template <bool SUB = false> struct TileIn {
 // Decoder 2: the sums inA = f64(Lc_A[perm[k]]) + Le1_A[perm[k]] (:511-516)
 // gathered from decoder 1's pre-summed output P1 (P1[j] = f64(Lc_A[j]) +
 // Le1_A[j], the same f64 addition), parities from Z = [N][64] float2 {W2, Y2}.
-template <bool SUB = false> struct TileInPre {
+struct TileInPre {
     const float2 *Z;
     const double2 *P;
     const int *p_idx;
     int lane;
     unsigned rs;
-    int xl = 0;    // SUB: the lane's plane offset (float2 units)
-    static constexpr bool SUBT = SUB;
-    __device__ __forceinline__ int xlane() const { return SUB ? xl : lane; }
     __device__ __forceinline__ Raw load(int k) const {
         Raw r;
-        const float2 z = at(Z, k * WAVE + xlane());
+        const float2 z = at(Z, k * WAVE + lane);
         r.v = make_float4(0.0f, 0.0f, z.x, z.y);
         r.l = at(P, wsrow(p_idx[k], rs) + lane);
         return r;
@@ -537,7 +551,7 @@ template <bool SUB = false> struct TileInPre {
     // {W2, Y2} as two 4-B planes inside the v slot, the gathered P1 in the l slot
     __device__ __forceinline__ void stage(int k, const LdsStage &st, int j) const {
         lds_f1 *dst = reinterpret_cast<lds_f1 *>(st.v + j * WAVE);
-        const unsigned zo = (unsigned)(k * WAVE + xlane()) * 8u;
+        const unsigned zo = (unsigned)(k * WAVE + lane) * 8u;
         glds4s(Z, zo, dst);
         glds4s(Z, zo + 4u, dst + WAVE);
         glds16s(P, (wsrow(p_idx[k], rs) + lane) * 16u, st.l + j * WAVE);
@@ -552,6 +566,12 @@ template <bool SUB = false> struct TileInPre {
     __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
 };
 
+#ifndef TDEC_OOR_STORE
+#define TDEC_OOR_STORE 0
+#endif
+#ifndef TDEC_LASTW_SKIP
+#define TDEC_LASTW_SKIP 0
+#endif
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
 // iteration) Le1 itself for the final decision (:529-530).
 // P1[k] is read by decoder 2 only as P1[perm[k']]: perm is not a permutation
@@ -574,11 +594,23 @@ struct TileOutPre {
     // other 53 % (N = 752) is dead.  Wave-uniform (scalar load).
     __device__ __forceinline__ bool need(int k) const { return Le || used[k]; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
+#if TDEC_OOR_STORE
+        // (round-6 A/B) discarded stores as buffer stores whose
+        // resource has num_records 0: the hardware drops them (no sink-row bytes),
+        // and they count in vmcnt like the sink stores, so the waits stay exact
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const bool kp = used[k];
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(&at(P, wsrow(k, rs)), 0, kp ? 0x7fffffff : 0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(Le ? &at(Le, wsrow(k, rs)) : P, 0, Le ? 0x7fffffff : 0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_double2((double)lcA + a, (double)lcB + b)), rp, lane * 16, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_double2(a, b)), rl, lane * 16, 0, 0);
+#else
         // wave-uniform row selects (SGPR pairs), then the lane offset
         double2 *rp = used[k] ? &at(P, wsrow(k, rs)) : sink;
         double2 *rl = Le ? &at(Le, wsrow(k, rs)) : sink;
         at(rp, (unsigned)lane) = make_double2((double)lcA + a, (double)lcB + b);
         at(rl, (unsigned)lane) = make_double2(a, b);
+#endif
     }
 };
 
@@ -1070,9 +1102,15 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             lcB[j] = rt[j].v.y;
         }
     }
+    // TDEC_LASTW_SKIP (round-6 A/B): the last window (k0 < 8) skips
+    // its prefetch of the next window, which would re-read its own rows
+    const bool lastw = TDEC_LASTW_SKIP && k0 < 8;   // wave-uniform
+    if (!lastw) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
-    in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
+        for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
+    }
+    if (lastw) wait_vm<0>();
+    else in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
     // (Keeping alpha[k0+2], passed on the way to alpha[k0+4], for the bottom half's
     // midpoint measured slower: profiles/r03w/, 250.9 vs 244.2 ms per 1 M codewords,
     // configs[1] 14.0 vs 10.4 ms -- the 16 registers it holds across the top half
@@ -1087,10 +1125,12 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             in.template gamma<ALGO>(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
         }
+        if (!lastw) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
+            for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
+        }
         window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
-    } else {
+    } else if (!lastw) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
     }
@@ -1108,7 +1148,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     // write, and the compiler's wait-count pass cannot see the asm DMA.  a0 is
     // needed at once by the bottom half, so the wait costs nothing.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
+    if (!lastw) ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
     window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
@@ -1219,7 +1259,6 @@ __device__ void siso8(const In &in, const Out &out, int N, float4 *ck, float4 *r
         In inp = in;
         int lanep = lane;
         asm volatile("" : "+v"(inp.lane), "+v"(lanep));
-        if constexpr (In::SUBT) asm volatile("" : "+v"(inp.xl));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             raw[j] = inp.load(RAG ? min(top + 4 + j, N - 1) : top + 4 + j);
@@ -1336,7 +1375,6 @@ struct DecodeArgs {
     // graph keeps its tail_seq, so on replay the gate finds the flag already raised.
     unsigned *tail_flag = nullptr;
     unsigned tail_seq = 0;
-    int unit_cw = WAVE;      // codewords per work unit (64, or T < 64 with sub-tiles)
 };
 
 // DVBRCS2_Turbo.decode (:464-537) for 64 codewords per wave, persistent over tiles.
@@ -1369,15 +1407,13 @@ __device__ int g_wave_tiles[WT_MAX];
 __device__ unsigned g_wave_hw[WT_MAX][2];   // HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID of each wave
 #endif
 
-// Work units.  Normally a unit is one 64-codeword plane tile (unit_cw = 64).  SUB
-// (sub-tiles): a batch of less than one round of resident waves x 64 codewords gives
-// every resident wave one unit of T = ceil(B / waves) < 64 codewords, so every
-// SIMD holds two equally loaded waves instead of some two full ones and some one
-// (configs[1]: 1 600 tiles on 2 048 wave slots).  A unit's
-// codewords [u T, u T + T) may straddle two plane tiles: each lane addresses the
-// planes by a virtual lane from the first tile's base (idle lanes >= T mirror the
-// unit's last codeword and write nothing).
-template <int ALGO, bool RAG, bool STAGED = false, bool SUB = false, class Pro = PlanesIn>
+// One tile = 64 codewords, one per lane.  (Sub-tile units -- every resident wave
+// one unit of ceil(B / waves) < 64 codewords when a batch has more tiles than SIMDs
+// but fewer than resident waves, so every SIMD holds two equally loaded waves --
+// measured slower at configs[1]: 10.74 vs 9.65 ms per 102 400 codewords, the clock
+// 1.68 vs 1.83 GHz: the extra waves' instruction streams cost more power than the
+// balance saved, profiles/r06a/, DESIGN.md appendix.)
+template <int ALGO, bool RAG, bool STAGED = false, class Pro = PlanesIn>
 __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const int *__restrict__ perm,
                                                    const int *__restrict__ inv, const int *__restrict__ used,
                                                    float4 *lv, double2 *ll,
@@ -1433,32 +1469,19 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             if (p.tail_flag && lane == 0 && (p.tile_ctr ? !has_next : tile == p.n_tiles - 1))
                 atomicMax(p.tail_flag, p.tail_seq);
         }
-        const int T = SUB ? p.unit_cw : WAVE;
-        const long c0 = (long)tile * T;                 // the unit's first codeword
-        int xl = lane, zl = lane;
-        const float *base;
-        if constexpr (SUB) {
-            const long t0 = c0 >> 6;
-            const long cl = min(c0 + min(lane, T - 1), (long)p.B - 1);   // inside the planes' tiles
-            const int dt = (int)((cl >> 6) - t0);
-            xl = (int)(cl & 63) + dt * N * 96;        // float4s per plane tile: N * 64 * 6 / 4
-            zl = (int)(cl & 63) + dt * N * 192;       // float2s per plane tile
-            base = pro.tile_planes((int)t0, wave, N, buf);
-        } else {
-            base = pro.tile_planes(tile, wave, N, buf);
-        }
+        const float *base = pro.tile_planes(tile, wave, N, buf);
         const float4 *X = reinterpret_cast<const float4 *>(base);
         const float2 *Z = reinterpret_cast<const float2 *>(base + NW * 4);
         {
             const double sf = it < p.iters - 1 ? 0.7 : 1.0;     // :496
             const bool last = it == p.iters - 1;
-            run_siso<ALGO, RAG, STAGED>(TileIn<SUB>{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u, xl},
+            run_siso<ALGO, RAG, STAGED>(TileIn{X, it ? Le2 : p.aux, inv, lane, it ? rs : 0u},
                                         TileOutPre{P1, last ? Le1 : nullptr, lane, rs, used, sink}, N, ck, ring, rs,
                                         lane, sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it, 2 * p.iters);
-            run_siso<ALGO, RAG, STAGED>(TileInPre<SUB>{Z, P1, perm, lane, rs, zl}, TileOut{Le2, lane, rs}, N, ck, ring,
-                                        rs, lane, sf, lv, ll, pr);
+            run_siso<ALGO, RAG, STAGED>(TileInPre{Z, P1, perm, lane, rs}, TileOut{Le2, lane, rs}, N, ck, ring, rs, lane,
+                                        sf, lv, ll, pr);
             pr.prog += PRIO_UNITS;
             if (has_next) pro.fill(nxt, wave, N, buf ^ 1, 2 * it + 1, 2 * p.iters);
         }
@@ -1472,8 +1495,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
         // writes the 64 rows chunk by chunk in row order (16-B int4 stores, each
         // wave store one contiguous 1 KiB run) instead of one 8-B store per lane
         // per couple 6 KB apart.
-        const long cw = c0 + lane;
-        const bool lane_on = lane < T && cw < p.B;
+        const long cw = (long)tile * WAVE + lane;
+        const bool lane_on = cw < p.B;
         uint32_t *hb = epi + (threadIdx.x >> 6) * epi_stride;
         const long nb = 2L * N;
         for (int kc = 0; kc < N; kc += 32) {
@@ -1488,7 +1511,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int k = min(kc + kg + u, N - 1);   // past the chunk: a valid row, unused
-                    const float4 x = at(X, k * WAVE + xl);
+                    const float4 x = at(X, k * WAVE + lane);
                     xa[u] = make_float2(x.x, x.y);
                     la[u] = at(Le2, wsrow(inv[k], rs) + lane);
                     le[u] = at(Le1, wsrow(k, rs) + lane);
@@ -1514,8 +1537,8 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
             const int per = (2 * kn + 3) / 4;
             for (int t = lane; t < WAVE * per; t += WAVE) {
                 const int l = t / per, pc = t - l * per;
-                const long row = c0 + l;
-                if (l >= T || row >= p.B) continue;
+                const long row = (long)tile * WAVE + l;
+                if (row >= p.B) continue;
                 const uint32_t w = hb[(pc >> 3) * WAVE + l] >> (4 * (pc & 7));
                 const int j = 4 * pc;                          // first int32 of the piece within the chunk
                 int32_t *dst = p.bits + row * nb + 2L * kc + j;
@@ -1566,19 +1589,13 @@ __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_W
     turbo_decode_tiles<0, RAG, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv), PlanesIn{p.planes},
                                      EPI_STRIDE_ML);
 }
-// The same decoder over sub-tile work units (turbo_decode_tiles, SUB).
-template <bool RAG>
-__global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_sub(
-    DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
-    __shared__ float4 lv[LDS_LV];
-    __shared__ double2 ll[LDS_STAGE];
-    turbo_decode_tiles<0, RAG, true, true>(p, perm, inv, used, lv, ll, reinterpret_cast<uint32_t *>(lv),
-                                           PlanesIn{p.planes}, EPI_STRIDE_ML);
-}
 template <bool RAG>
 __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
+#if TDEC_LM_LUT
+    lm_lut_fill();
+#endif
     turbo_decode_tiles<1, RAG>(p, perm, inv, used, nullptr, nullptr, epi, PlanesIn{p.planes});
 }
 

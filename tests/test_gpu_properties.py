@@ -154,12 +154,12 @@ def test_ragged_checkpoint_windows_full_size(n, mod):
 
 
 @pytest.mark.parametrize("n,mod,B", [(212, "QPSK", 102_400), (220, "16QAM", 100_003), (752, "16QAM", 70_001)])
-def test_sub_tile_units_vs_oracle(n, mod, B):
+def test_one_round_batches_vs_oracle(n, mod, B):
     """Batches of more 64-codeword tiles than SIMDs but fewer than resident waves
-    run sub-tile units (every resident wave one unit of ceil(B / waves) < 64
-    codewords): configs[1]'s shape, a ragged N whose units
-    straddle plane tiles and end in a partial unit, and N = 752 -- 4 096 rows
-    against the oracle, bits and L_final, and deterministic."""
+    (one round of the tile loop, some SIMDs with two waves and some with one):
+    configs[1]'s shape, a ragged N with a partial last tile, and N = 752 -- 4 096
+    rows against the oracle, bits and L_final.  (These batch shapes were the test
+    of round 6's sub-tile units, which lost and were removed.)"""
     dev = torch.device("cuda", 0)
     codec = M.DVBRCS2_Turbo(n, "1/3")
     _, syms, n0 = make_symbols(codec, B, mod, 1.5, 23, dev, want_info=False)

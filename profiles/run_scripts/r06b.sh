@@ -22,6 +22,6 @@ done
 for v in base lut; do
   lib=$L/libtdec.so; [ $v = base ] || lib=$L/libtdec_$v.so
   tools/profile.sh r06b/prof_c3_$v python tools/ab.py $lib --rounds 1 --n 752 --rate 1/2 --mod 8PSK --algo 1 > $O/prof_c3_$v.log 2>&1 || exit 1
-  timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_LDS -d $O/prof_c3_${v}_lds -o l --output-format csv -- python tools/ab.py $lib --rounds 1 --n 752 --rate 1/2 --mod 8PSK --algo 1 > $O/prof_c3_${v}_lds.log 2>&1 || true
+  timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS -d $O/prof_c3_${v}_lds -o l --output-format csv -- python tools/ab.py $lib --rounds 1 --n 752 --rate 1/2 --mod 8PSK --algo 1 > $O/prof_c3_${v}_lds.log 2>&1 || true
 done
 echo r06b done

@@ -84,20 +84,30 @@ def parse_points(spec):
     return [float(x) for x in spec.split(",")]
 
 
-def run_point(pipe, codec, mod, ebn0, start, count, batch, seed, device):
+def run_point(pipe, codec, mod, ebn0, start, count, batch, seed, device, times=None):
     """Bit errors, frame errors and codewords of global codewords
     [start, start + count) at one Eb/N0 point.  The data of codeword g is a
     counter-based stream of (seed, g) (workload.make_symbols), so the counters
-    do not depend on the batch size or on how the job is sharded."""
+    do not depend on the batch size or on how the job is sharded.  times (a list,
+    optional): per batch, (demap + decode ms, decode ms) from HIP events on the
+    pipeline's stream -- the bench's timed step, without the generator and the
+    error counting."""
     import torch
     from . import sharding as S
     from .workload import count_errors, make_symbols
     cnt = torch.zeros(3, dtype=torch.int64, device=device)
+    ev = []
     for off, n in S.batches(count, batch):
         _, syms, n0 = make_symbols(codec, n, mod, ebn0, seed, device, cw0=start + off, want_info=False)
-        bits = pipe.run(syms, n0)[:n]
+        e3 = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e3[0].record()
+        bits = pipe.run(syms, n0, events=e3[1:])[:n]
+        ev.append(e3)
         e = count_errors(codec, bits, seed, cw0=start + off)
         cnt += torch.stack([e.sum(dtype=torch.int64), (e > 0).sum(), torch.tensor(n, device=device)]).to(torch.int64)
+    if times is not None:
+        torch.cuda.synchronize()
+        times += [(a.elapsed_time(c), b.elapsed_time(c)) for a, b, c in ev]
     return cnt
 
 
@@ -153,12 +163,16 @@ def main(argv=None):
         S.check_same_interleaver(codec.inv_perm, dist, device if a.dist_backend == "nccl" else "cpu")
     pipe = DevicePipeline(codec, a.mod, a.batch, device)
     results = list(done.values())
+    # one untimed batch first: code-object loading and first-launch costs stay out of
+    # the first point's figures
+    run_point(pipe, codec, a.mod, 2.0, 0, min(a.batch, 65536), a.batch, a.seed, device)
     for e in parse_points(a.ebn0):
         if e in done:
             continue
         start, count = S.shard_range(a.codewords, world, rank)
         t0 = time.time()
-        cnt = run_point(pipe, codec, a.mod, e, start, count, a.batch, ebn0_seed(a.seed, e), device)
+        times = []
+        cnt = run_point(pipe, codec, a.mod, e, start, count, a.batch, ebn0_seed(a.seed, e), device, times)
         if world > 1 and a.dist_backend != "nccl":
             cnt = cnt.cpu()
         S.reduce_counters(cnt, dist if world > 1 else None)
@@ -168,7 +182,11 @@ def main(argv=None):
         rec = {"ebn0_db": e, "mod": a.mod, "n_couples": a.n, "rate": a.rate, "algo": a.algo,
                "interleaver": a.interleaver, "codewords": ncw,
                "bit_errors": be, "frame_errors": fe, "ber": be / (ncw * codec.k_info), "fer": fe / ncw,
-               "seconds": dt, "codewords_per_s": ncw / dt, "gpus": world}
+               "seconds": dt, "codewords_per_s": ncw / dt, "gpus": world,
+               # this rank's demap + decode (the bench's step) and decode alone, HIP events
+               "step_ms": sum(t[0] for t in times), "decode_ms": sum(t[1] for t in times),
+               "step_codewords_per_s": count / max(1e-9, sum(t[0] for t in times) * 1e-3),
+               "decode_codewords_per_s": count / max(1e-9, sum(t[1] for t in times) * 1e-3)}
         results.append(rec)
         if rank == 0:
             print(json.dumps(rec), flush=True)

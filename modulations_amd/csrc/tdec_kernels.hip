@@ -128,31 +128,12 @@ __device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf
 
 typedef float f2 __attribute__((ext_vector_type(2)));   // v_pk_add_f32 / v_pk_fma_f32 / v_pk_mul_f32: two IEEE f32 ops per lane
 
-// TDEC_LM_LUT (round-6 timing experiment, DIFFERENT BITS): the
-// correction log2(1 + 2^-d) from an LDS table of {value, slope} on a 1/256 grid of
-// d in [0, 24) (48 KiB, filled by k_turbo_decode_logmap), linear interpolation:
-// d * 256, cvt, min, fract, ds_read_b64, fma instead of the two transcendentals.
-#ifndef TDEC_LM_LUT
-#define TDEC_LM_LUT 0
-#endif
-#if TDEC_LM_LUT
-constexpr int LM_LUT_N = 24 * 256;
-__shared__ float2 g_lm_lut[LM_LUT_N];
-__device__ void lm_lut_fill() {
-    for (int i = threadIdx.x; i < LM_LUT_N; i += blockDim.x) {
-        const float v0 = hw_log2(1.0f + hw_exp2(-(float)i / 256.0f)), v1 = hw_log2(1.0f + hw_exp2(-(float)(i + 1) / 256.0f));
-        g_lm_lut[i] = make_float2(v0, v1 - v0);
-    }
-    __syncthreads();
-}
-#endif
+// (A correction log2(1 + 2^-d) from an LDS table -- {value, slope} on a 1/256 grid
+// of d in [0, 24), linear interpolation: d * 256, cvt, min, fract, ds_read_b64, fma
+// in place of the two transcendentals -- measured 14 % slower at configs[3]: 141.5
+// vs 123.8 ms per 262 144 codewords, +23 % VALU instructions and 4.1e9 LDS reads
+// with 5 bank-conflict cycles each, profiles/r06/b/, round 6.)
 __device__ __forceinline__ float jac(float a, float b) {
-#if TDEC_LM_LUT
-    const float x = fabsf(a - b) * 256.0f;
-    const unsigned i = min((unsigned)x, (unsigned)(LM_LUT_N - 1));
-    const float2 e = g_lm_lut[i];
-    return fmaxf(a, b) + fmaf(e.y, __builtin_amdgcn_fractf(x), e.x);
-#endif
     const float t = fabsf(a - b) + LM_C;
     const float w = fmaf(hw_exp2(-t), LM_SCALE, 1.0f);
     return fmaxf(a, b) + hw_log2(w);
@@ -566,12 +547,6 @@ struct TileInPre {
     __device__ __forceinline__ void wait_staged() const { wait_vm<12>(); }   // 4 x (2 x W2/Y2 + P1)
 };
 
-#ifndef TDEC_OOR_STORE
-#define TDEC_OOR_STORE 0
-#endif
-#ifndef TDEC_LASTW_SKIP
-#define TDEC_LASTW_SKIP 0
-#endif
 // Decoder 1's output: P1 = f64(Lc) + Le1 for decoder 2, and (last
 // iteration) Le1 itself for the final decision (:529-530).
 // P1[k] is read by decoder 2 only as P1[perm[k']]: perm is not a permutation
@@ -582,7 +557,10 @@ struct TileInPre {
 // A discarded store goes to the wave's sink row (L2-resident) instead of being
 // skipped: every position issues the same stores, so the count of memory
 // operations between a load and its use is the same on every path and the
-// compiler's s_waitcnt does not wait for stores it need not.
+// compiler's s_waitcnt does not wait for stores it need not.  (Dropping the
+// discarded stores instead -- buffer stores through a resource with num_records 0
+// -- cut 16 KB of the 1.18 MB per codeword and measured neutral, the clock
+// unchanged at 1.66-1.68 GHz: profiles/r06/b/, round 6.)
 struct TileOutPre {
     double2 *P, *Le;   // Le may be null
     int lane;
@@ -594,23 +572,11 @@ struct TileOutPre {
     // other 53 % (N = 752) is dead.  Wave-uniform (scalar load).
     __device__ __forceinline__ bool need(int k) const { return Le || used[k]; }
     __device__ __forceinline__ void store(int k, double a, double b, float lcA, float lcB) const {
-#if TDEC_OOR_STORE
-        // (round-6 A/B) discarded stores as buffer stores whose
-        // resource has num_records 0: the hardware drops them (no sink-row bytes),
-        // and they count in vmcnt like the sink stores, so the waits stay exact
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        const bool kp = used[k];
-        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(&at(P, wsrow(k, rs)), 0, kp ? 0x7fffffff : 0, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(Le ? &at(Le, wsrow(k, rs)) : P, 0, Le ? 0x7fffffff : 0, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_double2((double)lcA + a, (double)lcB + b)), rp, lane * 16, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, make_double2(a, b)), rl, lane * 16, 0, 0);
-#else
         // wave-uniform row selects (SGPR pairs), then the lane offset
         double2 *rp = used[k] ? &at(P, wsrow(k, rs)) : sink;
         double2 *rl = Le ? &at(Le, wsrow(k, rs)) : sink;
         at(rp, (unsigned)lane) = make_double2((double)lcA + a, (double)lcB + b);
         at(rl, (unsigned)lane) = make_double2(a, b);
-#endif
     }
 };
 
@@ -1102,15 +1068,11 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             lcB[j] = rt[j].v.y;
         }
     }
-    // TDEC_LASTW_SKIP (round-6 A/B): the last window (k0 < 8) skips
-    // its prefetch of the next window, which would re-read its own rows
-    const bool lastw = TDEC_LASTW_SKIP && k0 < 8;   // wave-uniform
-    if (!lastw) {
+    // (The last window re-reads its own rows here: skipping that saves 4 KB per
+    // codeword, L2-resident anyway, and measured neutral, profiles/r06/b/.)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
-    }
-    if (lastw) wait_vm<0>();
-    else in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
+    for (int j = 0; j < 4; ++j) in.stage(RAG ? min(kn + j, N - 1) : kn + j, sn, j);
+    in.wait_staged();   // + 4 for the checkpoint DMA, issued before the stage just above
     // (Keeping alpha[k0+2], passed on the way to alpha[k0+4], for the bottom half's
     // midpoint measured slower: profiles/r03w/, 250.9 vs 244.2 ms per 1 M codewords,
     // configs[1] 14.0 vs 10.4 ms -- the 16 registers it holds across the top half
@@ -1125,12 +1087,10 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
             in.template gamma<ALGO>(in.staged(st, i), g, x, y);
             alpha_step<ALGO>(a4, g);
         }
-        if (!lastw) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
-        }
+        for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
         window_half<ALGO, RAG>(out, k0 + 4, lenT, a4, gw, iAw, iBw, lcA, lcB, b, sf);
-    } else if (!lastw) {
+    } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) rt[j] = in.load(RAG ? min(kn + 4 + j, N - 1) : kn + 4 + j);
     }
@@ -1148,7 +1108,7 @@ __device__ __forceinline__ void back_window8(const In &in, const Out &out, int k
     // write, and the compiler's wait-count pass cannot see the asm DMA.  a0 is
     // needed at once by the bottom half, so the wait costs nothing.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!lastw) ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
+    ck_stage(ck, cs, (kn / 8) * 4, lane, st.ck);
     window_half<ALGO, RAG>(out, k0, lenB, a0, gw, iAw, iBw, lcA, lcB, b, sf);
 }
 
@@ -1593,9 +1553,6 @@ template <bool RAG>
 __global__ __launch_bounds__(DEC_BLOCK) __attribute__((amdgpu_waves_per_eu(DEC_WPE))) void k_turbo_decode_logmap(
     DecodeArgs p, const int *__restrict__ perm, const int *__restrict__ inv, const int *__restrict__ used) {
     __shared__ uint32_t epi[DEC_WAVES * 2 * WAVE];
-#if TDEC_LM_LUT
-    lm_lut_fill();
-#endif
     turbo_decode_tiles<1, RAG>(p, perm, inv, used, nullptr, nullptr, epi, PlanesIn{p.planes});
 }
 

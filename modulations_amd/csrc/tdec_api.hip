@@ -1052,7 +1052,7 @@ int tdec_decode_planes_dev(tdec_t *h, int B, const float *d_planes, int32_t *d_b
     if (waves > h->ws_waves) return fail(TDEC_ECAPACITY, "workspace too small: call tdec_reserve first");
     if (int rc = order_on(h, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, d_planes, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used,
-                 h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
+                 waves * WAVE, h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     if (h->d_simd_prog && hipMemsetAsync(h->d_simd_prog, 0, SIMD_PROG_BYTES, st) == hipSuccess) a.simd_prog = h->d_simd_prog;
     a.tail_flag = h->d_tail;
     a.tail_seq = ++h->tail_seq;
@@ -1829,7 +1829,7 @@ int tdec_demap_decode_dev(tdec_t *h, int B, const float *d_syms, int S, const vo
     if (int rc = order_on(h, st)) return rc;
     if (int rc = h->cons.upload(cons, cons_f64, M, bps, cons_f64 != 0, st)) return rc;
     DecodeArgs a{B, h->N, h->iters, tiles, waves, nullptr, h->le_p, h->ck_p, d_bits, d_lfinal, h->d_used,
-                 h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
+                 waves * WAVE, h->aux_p, tile_queue(h, tiles, waves, st), ck_rows_of(h)};
     FusedDemapArgs fa{d_syms, S, std::min<long>((long)S * bps, h->llr_len), (const int *)h->d_src,
                       (const int *)h->d_off, (float *)h->planes_w.p,
                       demap_cfg(M, div_f32, -1, noise_var, h->cons.sep), h->cons.buf.p};

@@ -1351,6 +1351,10 @@ struct DecodeArgs {
     int32_t *bits;           // [B][2N]
     double *lfinal;          // [B][2N] or null
     const int *p1_used;      // [N]: 1 where k is in the image of perm (P1 rows decoder 2 reads)
+    // workspace row stride in lanes (= n_waves * 64, set by the host): opaque to the
+    // compiler, which otherwise proves it a multiple of 64 and forms every lane
+    // offset with v_lshlrev + v_or instead of one v_add_lshl_u32 (+1.5 % decode time)
+    int row_lanes;
     double2 *aux;            // [64] zeros (the first iteration's a-priori), then one sink row per wave
     int *tile_ctr;           // null: static tile striding; else a zeroed counter (dynamic tile queue)
     int ck_rows;             // checkpoint rows before the beta1 ring: ceil(N / ck_win_of(algo))
@@ -1414,7 +1418,7 @@ __device__ __forceinline__ void turbo_decode_tiles(const DecodeArgs &p, const in
     const int N = p.N;
     const long NW = (long)N * WAVE;
     // workspace rows interleave the waves: [plane][k][wave][64] and [slot][wave][64]
-    const unsigned rs = (unsigned)p.n_waves * WAVE;
+    const unsigned rs = (unsigned)p.row_lanes;
     double2 *P1 = p.ws + (long)wave * WAVE * WS_G, *Le2 = P1 + (long)rows_of(N) * rs, *Le1 = Le2 + (long)rows_of(N) * rs;
     const int nw = p.ck_rows;
     float4 *ck = p.ck + (long)wave * WAVE * WS_G;

@@ -58,9 +58,6 @@ __host__ __device__ constexpr int t_prev_i(int ns, int idx) {
 // instead of 0.5 (see the log-MAP section below).
 constexpr double LM_K = 0x1.71547652b82fep-1;     // 0.5 * log2(e)
 constexpr double LM_LN2 = 0x1.62e42fefa39efp-1;   // ln 2: bits -> nats
-#ifndef TDEC_LM_X16
-#define TDEC_LM_X16 0
-#endif
 // log-MAP (ALGO 1, round 4) uses the branch metric's two halves instead:
 // g = {U0, U1, V0, V1, 0...} with U0 = f32(hA + hB), U1 = f32(hA - hB),
 // V0 = f32(hW + hY), V1 = f32(hW - hY) (f64 sums rounded once, weights in bits):
@@ -354,33 +351,9 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
         // regrouped: u = alpha[s] + beta[next(s, c)] per input class c, summed per
         // parity pair wy over its 4 states (V), then the 4 branch metrics of the
         // input on top (the gamma of a branch depends only on the input and wy).
-        float X[2];
-#if TDEC_LM_X16
-        // (round-6 timing experiment, DIFFERENT BITS) X_c as one log-sum over the 16
-        // states instead of two levels of lse4: 16 exp + 1 log instead of 20 + 5
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            float x[16];
-#pragma unroll
-            for (int wy = 0; wy < 4; ++wy)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int st = LM_GROUPS.s[c][wy][i];
-                    x[wy * 4 + i] = (a[st] + b1[t_next(st, c)]) + lm_v(g, wy);
-                }
-            float M = x[0];
-#pragma unroll
-            for (int i = 1; i < 16; ++i) M = fmaxf(M, x[i]);
-            const float Mc = M + LM_C;
-            float S = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) S = fmaf(hw_exp2(-(Mc - x[i])), 128.0f, S);
-            X[c] = (Mc - LM_C) + (hw_log2(S) + 1.0f);
-        }
-        if (false) {
-#else
-        {
-#endif
+        // (One log-sum over the 16 states per input class instead of two levels of
+        // lse4 -- 16 exp + 1 log instead of 20 + 5 -- measured 1.6 % faster at
+        // configs[3], profiles/r06/d/: too little to redefine the build's log-MAP.)
         float V[2][4];
 #pragma unroll
         for (int c = 0; c < 2; ++c)
@@ -399,10 +372,10 @@ __device__ __forceinline__ void extrinsic(const float (&a)[NS], const float (&g)
             }
         // app[inp] = +-U_c + X_c, X_c = lse4 over wy of (v(wy) + V[c][wy]): the two
         // inputs of a class share X_c (round 4; round 3 took one lse4 per input)
+        float X[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c)
             X[c] = lse4(lm_v(g, 0) + V[c][0], lm_v(g, 1) + V[c][1], lm_v(g, 2) + V[c][2], lm_v(g, 3) + V[c][3]);
-        }
         const float app[4] = {g[0] + X[0], g[1] + X[1], -g[1] + X[1], -g[0] + X[0]};
         LpA = jac(app[0], app[1]) - jac(app[2], app[3]);
         LpB = jac(app[0], app[2]) - jac(app[1], app[3]);
